@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""bench.py -- distinct states/sec to exhaust a bounded 3-server Raft model.
+
+A "step" is one complete model check of the workload: clear the fingerprint
+set, Init, then BFS levels until no new state (TLC's "0 states left on
+queue").  value = distinct states / mean wall time per step, the wall time
+to exhaust being ms_per_step.  All inputs are device-resident (the search
+starts from the Init row); nothing crosses PCIe inside a level except an
+~100-byte counter read-back.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+N > 1 (launched by torch.distributed.run): each rank checks the full model
+independently ("replicas") until the fingerprint-sharded path lands; the
+line says so in config.parallelism.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raft-tla_amd"))
+
+# Feasible analogues of BASELINE.json configs (the reference's bounds give
+# >1e11 states): name -> (N, V, MaxTerm, MaxLogLen, MaxCopies, MaxInFlight, invariants)
+WORKLOADS = {
+    "raft3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, ("ElectionSafety", "LogMatching")),
+    "raft3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, ("NoTwoLeaders",)),
+    "raft3_v1_t2_l1_m1": (3, 1, 2, 1, 1, 1, ("NoTwoLeaders",)),
+}
+DEFAULT = "raft3_v2_t2_l1_m2"
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def dist_env():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def cpu_baseline(shape, sample_states, threads):
+    """The C oracle (oracle/raft_cpu.c, a 'port' of the spec) on a bounded
+    prefix of the same BFS: distinct states/s on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import raft_cpu
+    n, v, t, l, c, m, inv = shape
+    r = raft_cpu.bfs(raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=sample_states), threads=threads)
+    return {"value": r["distinct"] / r["seconds"], "unit": "distinct states/s", "cores": threads,
+            "kind": "port",
+            "sample": "oracle/raft_cpu.c BFS of the same model, first %d levels (%d distinct, %d generated) in %.1f s"
+                      % (len(r["levels"]), r["distinct"], r["generated"], r["seconds"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default=DEFAULT, choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-sample", type=int, default=12_000_000, help="states in the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--levels", action="store_true", help="print the per-level table to stderr")
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # control plane only (barriers, max-reduce of times)
+    import rtla
+
+    shape = WORKLOADS[args.workload]
+    n, v, t, l, c, m, inv = shape
+    cfg = rtla.Config(n, v, t, l, c, m, inv)
+    ck = rtla.Checker(cfg, rank=local, world=1)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def one_run():
+        ck.reset()
+        ck.run()
+        if ck.status < 0 or ck.status == rtla.VIOLATION:
+            raise SystemExit("model check ended with status %d" % ck.status)
+        return ck.levels
+
+    for _ in range(args.warmup):
+        one_run()
+    barrier()
+    t0 = time.perf_counter()
+    runs = []
+    for _ in range(args.steps):
+        runs.append(one_run())
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    levels = runs[-1]
+    distinct = sum(lv.new for lv in levels)
+    generated = sum(lv.generated for lv in levels)
+    depth = sum(1 for lv in levels if lv.new > 0)
+    per_step = elapsed / args.steps
+    value = distinct * world / per_step
+
+    # roofline of the dominant kernel (k_expand), from the last run's HIP-event times
+    S = levels[0].row_bytes
+    kms = sum(lv.kernel_ms for lv in runs[-1][1:])
+    launches = len(runs[-1]) - 1
+    E = sum(lv.frontier for lv in levels[1:])
+    D = sum(lv.new for lv in levels[1:])
+    P = sum(lv.probes for lv in levels[1:])
+    stream_bytes = E * S + D * (S + 8)
+    probe_bytes = P * 64
+    achieved = (stream_bytes + probe_bytes) / (kms / 1e3) / 1e9
+    if args.levels and rank == 0:
+        for lv in levels:
+            print("level %3d frontier %12d new %12d generated %13d kernel %9.3f ms" %
+                  (lv.level, lv.frontier, lv.new, lv.generated, lv.kernel_ms), file=sys.stderr)
+
+    out = {
+        "metric": "distinct states/sec (whole node) + wall time to exhaust, 3-server Raft",
+        "value": value,
+        "unit": "distinct states/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": per_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak" if world > 1 else "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "exhaustive BFS from Init (no input data)",
+        "config": {
+            "workload": args.workload,
+            "servers": n, "values": v, "max_term": t, "max_log": l, "max_copies": c, "max_in_flight": m,
+            "invariants": list(inv), "distinct": distinct, "generated": generated, "depth": depth,
+            "parallelism": "single" if world == 1 else "replicas%d" % world,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "k_expand", "launches": launches, "kernel_ms_total": kms,
+            "kernel_ms_avg": kms / max(1, launches),
+            "algorithmic_bytes": stream_bytes + probe_bytes,
+            "model": "E*S + D*(S+8) streamed + one 64-B transaction per fingerprint probe",
+            "probes_per_s": P / (kms / 1e3),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(shape, args.cpu_sample, args.cpu_threads)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ck.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * rtla.h -- C ABI of the MI355X-native Raft model checker (librtla.so).
+ *
+ * What this boundary replaces.  The reference (bernborgess/raft-tla) is a
+ * TLA+ spec run by TLC:
+ *     java tlc2.TLC [-workers W] [-coverage 1] -config raft.cfg raft.tla
+ * (/root/reference/raft.cfg:1-15 is the model, /root/reference/.vscode/
+ * settings.json:5 the "-coverage 1" option).  The hot path behind that command
+ * is TLC's breadth-first exploration of Spec == Init /\ [][Next]_vars
+ * (/root/reference/raft.tla:469, Next at :454-465): expand every frontier
+ * state, fingerprint each successor, deduplicate against the seen set, check
+ * invariants, enqueue.  Each entry point below replaces one piece of it:
+ *
+ *   rtla_open / rtla_close   TLC's model setup from the cfg's CONSTANTS
+ *                            (raft.cfg:5-15) and its FPSet / StateQueue
+ *                            allocation (the `states/` dir, reference
+ *                            .gitignore:2).
+ *   rtla_init                "Computing initial states" -- Init (raft.tla:155-160).
+ *   rtla_step                one BFS level of TLC's worker loop: Next
+ *                            (raft.tla:454-465), fingerprint, FPSet.put,
+ *                            INVARIANT check (raft.cfg:3), enqueue.
+ *   rtla_violation,
+ *   rtla_trace               "Error: Invariant X is violated" + "The behavior
+ *                            up to this point is:" (TLC's trace file).
+ *   rtla_coverage            "-coverage 1" (.vscode/settings.json:5): per-action
+ *                            generated / distinct counts.
+ *   rtla_expand_batch        TLC's Tool.getNextStates(Next, s) for a batch of
+ *                            states: the parity seam used by the tests.
+ *   rtla_state_text          TLC's state printer ("/\ var = value" lines).
+ *
+ * Conventions: the caller owns host buffers, the library owns device memory.
+ * Every function returns an int status (RTLA_OK = 0, >0 informational,
+ * <0 error).  Nothing is thrown across the ABI.  Capacity overflow of any
+ * fixed-width structure is a hard error (RTLA_E_OVERFLOW), never truncation.
+ * A context is used from one host thread; one context per GPU (rank).
+ */
+#ifndef RTLA_H
+#define RTLA_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTLA_ABI_VERSION 1
+
+/* status codes */
+#define RTLA_OK 0
+#define RTLA_DONE 1          /* the last level found no new state: search complete */
+#define RTLA_VIOLATION 2     /* an invariant is violated; see rtla_violation / rtla_trace */
+#define RTLA_E_CONFIG (-1)   /* configuration outside the supported row format */
+#define RTLA_E_HIP (-2)      /* HIP runtime error (no device, launch failure, OOM) */
+#define RTLA_E_OVERFLOW (-3) /* bag / elections / frontier / fingerprint-set capacity exceeded */
+#define RTLA_E_SPEC (-4)     /* TLC evaluation error while evaluating Next */
+#define RTLA_E_STATE (-5)    /* call out of order (e.g. step before init) */
+#define RTLA_E_ARG (-6)      /* bad argument / buffer too small */
+#define RTLA_E_COMM (-7)     /* RCCL error */
+
+/* invariants (definitions: specs/MC.tla) */
+#define RTLA_INV_NO_TWO_LEADERS 1
+#define RTLA_INV_ELECTION_SAFETY 2
+#define RTLA_INV_LOG_MATCHING 4
+
+typedef struct rtla_ctx rtla_ctx;
+
+typedef struct {
+    int32_t n_server;    /* |Server|                         (raft.cfg:6)  <= 5 */
+    int32_t n_value;     /* |Value|                          (raft.cfg:7)  <= 4 */
+    int32_t max_term;    /* StateConstraint: currentTerm <= max_term        <= 6 */
+    int32_t max_log;     /* StateConstraint: Len(log) <= max_log            <= 4 */
+    int32_t max_copies;  /* StateConstraint: messages[m] <= max_copies      <= 14 */
+    int32_t max_msgs;    /* StateConstraint: BagCardinality <= max_msgs; 0 = unbounded */
+    int32_t bag_cap;     /* distinct messages per row; 0 = auto (max_msgs + 1, or 32) */
+    int32_t elec_cap;    /* election records per row; 0 = auto ((max_term - 1) * n_server) */
+    int32_t inv_mask;    /* RTLA_INV_* */
+    int32_t symmetry;    /* must be 0 in this version */
+    int32_t fpset_log2;  /* log2(#8-byte slots) of this rank's fingerprint set; 0 = auto */
+    int32_t reserved;
+    uint64_t frontier_cap; /* states per frontier buffer; 0 = auto */
+    uint64_t mem_budget;   /* bytes of HBM this context may use; 0 = 85% of free */
+} rtla_cfg;
+
+typedef struct {
+    int32_t level;            /* BFS level whose states were just produced (Init = 1) */
+    int32_t status;           /* RTLA_OK / RTLA_DONE / RTLA_VIOLATION */
+    uint64_t frontier;        /* states expanded to produce this level */
+    uint64_t new_states;      /* distinct states first found at this level */
+    uint64_t generated;       /* successor states generated (incl. out-of-model) */
+    uint64_t distinct_total;  /* distinct states found so far (all ranks) */
+    uint64_t generated_total; /* states generated so far, Init included (TLC convention) */
+    double seconds;           /* wall time of this level (device work + sync) */
+    double kernel_ms;         /* k_expand time of this level (HIP events on the context's stream) */
+    uint64_t probes;          /* in-model successors (fingerprint-set probes) */
+    uint64_t row_bytes;       /* bytes of one packed state row */
+} rtla_level_stats;
+
+/* Library / context lifetime.  world > 1: `comm_id` is the 128-byte RCCL
+ * unique id shared by all ranks (rank 0 makes it with rtla_comm_id). */
+int rtla_open(const rtla_cfg *cfg, int rank, int world, const void *comm_id, rtla_ctx **out);
+void rtla_close(rtla_ctx *ctx);
+int rtla_comm_id(void *out128);
+
+/* BFS. */
+int rtla_init(rtla_ctx *ctx, rtla_level_stats *out);
+/* Forget the search (clear the fingerprint set, frontier, counters) but keep
+ * the allocations, so the same model can be checked again from Init. */
+int rtla_reset(rtla_ctx *ctx);
+int rtla_step(rtla_ctx *ctx, rtla_level_stats *out);
+int rtla_violation(rtla_ctx *ctx, int32_t *inv_mask, int32_t *in_model);
+/* Counterexample, Init first.  rows: n * rtla_row_words() u32; labels: action
+ * instance per state (-1 for Init).  *n_rows is set even if cap is too small. */
+int rtla_trace(rtla_ctx *ctx, uint32_t *rows, int32_t *labels, size_t cap, size_t *n_rows);
+/* Copy the current frontier (the states of the level last produced) to the
+ * host: *n = #states; rows needs n * rtla_row_words() u32. */
+int rtla_frontier(rtla_ctx *ctx, uint32_t *rows, size_t cap, size_t *n);
+/* gen/distinct per coverage code (10 families, Receive split in 6). */
+int rtla_coverage(rtla_ctx *ctx, uint64_t *gen, uint64_t *distinct, int n);
+int rtla_device_info(rtla_ctx *ctx, char *buf, size_t cap);
+
+/* Stateless helpers (need a GPU only for rtla_expand_batch). */
+int rtla_row_words(const rtla_cfg *cfg);
+int rtla_init_row(const rtla_cfg *cfg, uint32_t *row);
+/* Every enabled successor of each input row.  succ: cap rows; info[k] =
+ * input index << 32 | in_model << 31 | receive-sub << 16 | instance. */
+int rtla_expand_batch(const rtla_cfg *cfg, const uint32_t *rows, size_t n, uint32_t *succ,
+                      uint64_t *info, size_t cap, size_t *n_out);
+int rtla_state_text(const rtla_cfg *cfg, const uint32_t *row, char *buf, size_t cap);
+int rtla_action_name(const rtla_cfg *cfg, int32_t inst, int32_t sub, char *buf, size_t cap);
+int rtla_invariants(const rtla_cfg *cfg, const uint32_t *row);  /* violated mask */
+const char *rtla_strerror(int status);
+int rtla_abi_version(void);
+
+/* Calibration: n random 8-byte CAS inserts into a table of 2^log2 slots;
+ * returns device seconds. */
+int rtla_probe_bench(int log2, uint64_t n, double *seconds, uint64_t *inserted);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,35 @@
+// rtla_device.h -- structures shared by the kernels and the host driver.
+#pragma once
+#include <stdint.h>
+
+#include "rtla_model.h"
+
+namespace rtla {
+
+// Coverage codes: the 10 Next families, with Receive split into its 6
+// sub-actions (UpdateTerm, HandleRequestVoteRequest, HandleRequestVoteResponse,
+// HandleAppendEntriesRequest, HandleAppendEntriesResponse, DropStaleResponse).
+constexpr int COVER_CODES = F_COUNT + R_NONE;
+
+enum {
+  FLAG_SPEC_ERROR = 1,      // TLC evaluation error (sequence index outside its domain)
+  FLAG_ROW_OVERFLOW = 2,    // bag / elections capacity of the row format exceeded
+  FLAG_FRONTIER_FULL = 4,   // next-frontier buffer too small
+  FLAG_FPSET_FULL = 8,      // fingerprint set probe limit hit
+};
+
+// Per-level device counters (zeroed before each level except `cover`).
+struct DevCounters {
+  unsigned long long generated;
+  unsigned long long next_count;
+  unsigned long long probes;
+  int flags;
+  int viol_mask;
+  int viol_inst;
+  int viol_in_model;
+  unsigned long long viol_parent;
+  unsigned long long viol_child;
+  unsigned long long cover[2 * COVER_CODES];  // [0,C): generated, [C,2C): distinct
+};
+
+}  // namespace rtla

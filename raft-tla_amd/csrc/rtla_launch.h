@@ -1,0 +1,25 @@
+// rtla_launch.h -- host-side launch wrappers for the kernels in rtla_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rtla_device.h"
+
+namespace rtla {
+
+// LDS bytes a k_expand / k_expand_batch block of `wpb` waves needs.
+size_t expand_lds_bytes(const Layout& L, int wpb);
+// Blocks of 4 waves that fit on one CU given the LDS footprint.
+int expand_blocks_per_cu(const Layout& L);
+
+hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t n_cur, uint64_t cur_base,
+                         uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                         uint64_t* table, int tlog2, DevCounters* ctr, int grid, hipStream_t st);
+hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
+                              int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st);
+hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,
+                               uint64_t* info, uint64_t cap, DevCounters* ctr, hipStream_t st);
+hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed,
+                              DevCounters* ctr, hipStream_t st);
+
+}  // namespace rtla

@@ -1,0 +1,698 @@
+// rtla_model.h -- packed Raft state rows and the semantics of raft.tla's Next.
+//
+// This header is the ONE place where the spec's actions are written for the
+// product.  Every function is __host__ __device__: the GPU kernels
+// (rtla_kernels.hip) evaluate it per (state, action-instance) lane, and the
+// host driver uses the same code only to build Init and to decode rows to
+// text.  There is no CPU expansion path in the product.
+//
+// Reference: /root/reference/raft.tla (sha256 683a120a...6b81).  Each action
+// below cites the lines it follows.
+//
+// ---------------------------------------------------------------------------
+// Row layout (u32 words; all offsets from rtla::Layout):
+//   [0..4)            fingerprint (a.lo, a.hi, b.lo, b.hi) of this state
+//   [off_hdr]         nmsg (bits 0-7) | nelec (bits 8-15)
+//   [off_srv + i*SW]  server record i, SW = 3 + N words:
+//       w0 scalars:   currentTerm 0-3 | state 4-5 | votedFor 6-8 (7 = Nil)
+//                     | commitIndex 9-11 | votesResponded 12-16
+//                     | votesGranted 17-21 | DOMAIN voterLog[i] 22-26
+//       w1 log[i]     (log code, below)
+//       w2            nextIndex[i][j] at 3j | matchIndex[i][j] at 15+3j
+//       w3+j          voterLog[i][j] (log code; 0 unless bit j of the domain)
+//   [off_all]         allLogs: bitmask over the in-model log universe
+//   [off_elec + e*EW] elections, EW = 2 + N words, nelec records:
+//       w0 eterm 0-3 | eleader 4-6 | evotes 7-11 | DOMAIN evoterLog 12-16
+//       w1 elog, w2+j evoterLog[j]
+//   [off_bag + 2k]    message bag slot k (u64: key | count << 60), nmsg used
+//
+// Log code (u32): length in bits 0-2; entry k (0-based) at bits 3+5k:
+//   term (3 bits) | value << 3 (2 bits).
+// Message key (u64), fields by type (raft.tla:193-198, :215-225, :294-301, :338-343):
+//   type 0-1 | msource 2-4 | mdest 5-7 | mterm 8-11 |
+//   RVReq:  mlastLogTerm 12-15 | mlastLogIndex 16-18
+//   RVResp: mvoteGranted 12 | mlog 16-43
+//   AEReq:  mprevLogIndex 12-14 | mprevLogTerm 15-18 | has-entry 19 |
+//           entry 20-24 | mcommitIndex 25-27 | mlog 28-55
+//   AEResp: msuccess 12 | mmatchIndex 13-15
+//
+// The bag, the elections list and the bag slots are NOT kept in canonical
+// order.  State identity is decided only by the fingerprint, which is a sum
+// over the state's components (per-server records, messages with their
+// counts, allLogs members, election records) of a 128-bit PRF of each
+// component -- an order-free function of the TLA+ value.  Two distinct values
+// differ in at least one component, so they collide with probability 2^-128
+// per pair (2^-64 per half).
+// ---------------------------------------------------------------------------
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define RTLA_HD __host__ __device__ __forceinline__
+#else
+#define RTLA_HD static inline
+#endif
+
+namespace rtla {
+
+constexpr int NMAX = 5;   // servers
+constexpr int LMAX = 4;   // MaxLogLen (rows hold LMAX+1 entries)
+constexpr int TMAX = 6;   // MaxTerm (rows hold MaxTerm+1)
+constexpr int VMAX = 4;   // values
+constexpr int CMAX = 14;  // MaxCopies (rows hold MaxCopies+1)
+constexpr int KMAX = 64;  // bag slots
+constexpr int EMAX = 32;  // election records
+constexpr int WMAX = 4 + 1 + NMAX * (3 + NMAX) + 32 + EMAX * (2 + NMAX) + 2 * KMAX;
+
+enum { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
+enum { RVREQ = 0, RVRESP = 1, AEREQ = 2, AERESP = 3 };
+constexpr uint32_t NIL = 7;
+
+// Action families (instance ranges in Layout::fam).  Order = disjunct order of
+// Next (raft.tla:454-463).
+enum {
+  F_RESTART = 0, F_TIMEOUT, F_REQUESTVOTE, F_BECOMELEADER, F_CLIENTREQUEST,
+  F_ADVANCECOMMIT, F_APPENDENTRIES, F_RECEIVE, F_DUPLICATE, F_DROP, F_COUNT
+};
+// Receive sub-actions, reported for coverage / trace labels.
+enum {
+  R_UPDATETERM = 0, R_HRVREQ, R_HRVRESP, R_HAEREQ, R_HAERESP, R_DROPSTALE, R_NONE
+};
+
+// Invariant bits (build-defined model wrapper, oracle/MC.tla).
+enum { INV_NO_TWO_LEADERS = 1, INV_ELECTION_SAFETY = 2, INV_LOG_MATCHING = 4 };
+
+struct Layout {
+  int N, V, T, L, C, M, K, E;
+  int inv_mask;
+  int SW, EW;
+  int off_hdr, off_srv, off_all, all_words, off_elec, off_bag, W;
+  int n_logs;          // |{logs of length <= L, terms 1..T}|
+  int fam[F_COUNT + 1];  // first instance id of each family; fam[F_COUNT] = #instances
+  int log_off[LMAX + 2];  // allLogs index offset of logs of length n
+};
+
+// Returns 0 on success, <0 if the configuration exceeds the row format.
+static inline int make_layout(Layout* l, int N, int V, int T, int L, int C, int M, int K, int E,
+                              int inv_mask) {
+  if (N < 1 || N > NMAX || V < 1 || V > VMAX || T < 1 || T > TMAX || L < 0 || L > LMAX ||
+      C < 1 || C > CMAX || M < 0 || K < 1 || K > KMAX || E < 0 || E > EMAX)
+    return -1;
+  if (M > 0 && K < M + 1) return -1;  // out-of-model successors must stay representable
+  l->N = N; l->V = V; l->T = T; l->L = L; l->C = C; l->M = M; l->K = K; l->E = E;
+  l->inv_mask = inv_mask;
+  l->SW = 3 + N;
+  l->EW = 2 + N;
+  int B = T * V, off = 0, pw = 1;
+  for (int n = 0; n <= L + 1; n++) { l->log_off[n] = off; off += pw; pw *= B; }
+  l->n_logs = l->log_off[L + 1];
+  if (l->n_logs > 32 * 32) return -1;
+  l->off_hdr = 4;
+  l->off_srv = 5;
+  l->off_all = l->off_srv + N * l->SW;
+  l->all_words = (l->n_logs + 31) / 32;
+  l->off_elec = l->off_all + l->all_words;
+  l->off_bag = l->off_elec + E * l->EW;
+  l->off_bag += (l->off_bag & 1);  // u64-align the bag
+  l->W = l->off_bag + 2 * K;
+  l->W += !(l->W & 1);  // odd row stride: conflict-free LDS row staging
+  int f = 0;
+  l->fam[F_RESTART] = f; f += N;
+  l->fam[F_TIMEOUT] = f; f += N;
+  l->fam[F_REQUESTVOTE] = f; f += N * N;
+  l->fam[F_BECOMELEADER] = f; f += N;
+  l->fam[F_CLIENTREQUEST] = f; f += N * V;
+  l->fam[F_ADVANCECOMMIT] = f; f += N;
+  l->fam[F_APPENDENTRIES] = f; f += N * N;
+  l->fam[F_RECEIVE] = f; f += K;
+  l->fam[F_DUPLICATE] = f; f += K;
+  l->fam[F_DROP] = f; f += K;
+  l->fam[F_COUNT] = f;
+  return 0;
+}
+
+// ------------------------------------------------------------- fields ----
+RTLA_HD uint32_t s_term(uint32_t w) { return w & 15u; }
+RTLA_HD uint32_t s_role(uint32_t w) { return (w >> 4) & 3u; }
+RTLA_HD uint32_t s_voted(uint32_t w) { return (w >> 6) & 7u; }
+RTLA_HD uint32_t s_commit(uint32_t w) { return (w >> 9) & 7u; }
+RTLA_HD uint32_t s_vresp(uint32_t w) { return (w >> 12) & 31u; }
+RTLA_HD uint32_t s_vgrant(uint32_t w) { return (w >> 17) & 31u; }
+RTLA_HD uint32_t s_vlp(uint32_t w) { return (w >> 22) & 31u; }
+RTLA_HD uint32_t s_make(uint32_t term, uint32_t role, uint32_t voted, uint32_t commit,
+                        uint32_t vresp, uint32_t vgrant, uint32_t vlp) {
+  return term | role << 4 | voted << 6 | commit << 9 | vresp << 12 | vgrant << 17 | vlp << 22;
+}
+RTLA_HD uint32_t nm_next(uint32_t w, int j) { return (w >> (3 * j)) & 7u; }
+RTLA_HD uint32_t nm_match(uint32_t w, int j) { return (w >> (15 + 3 * j)) & 7u; }
+RTLA_HD uint32_t nm_set_next(uint32_t w, int j, uint32_t v) {
+  return (w & ~(7u << (3 * j))) | (v << (3 * j));
+}
+RTLA_HD uint32_t nm_set_match(uint32_t w, int j, uint32_t v) {
+  return (w & ~(7u << (15 + 3 * j))) | (v << (15 + 3 * j));
+}
+RTLA_HD uint32_t nm_fill(int N, uint32_t next, uint32_t match) {
+  uint32_t w = 0;
+  for (int j = 0; j < N; j++) w |= next << (3 * j) | match << (15 + 3 * j);
+  return w;
+}
+
+// Log codes
+RTLA_HD uint32_t log_len(uint32_t l) { return l & 7u; }
+RTLA_HD uint32_t log_entry(uint32_t l, uint32_t k1) { return (l >> (3 + 5 * (k1 - 1))) & 31u; }
+RTLA_HD uint32_t log_term(uint32_t l, uint32_t k1) { return log_entry(l, k1) & 7u; }
+RTLA_HD uint32_t log_val(uint32_t l, uint32_t k1) { return log_entry(l, k1) >> 3; }
+RTLA_HD uint32_t last_term(uint32_t l) { return log_len(l) ? log_term(l, log_len(l)) : 0u; }
+RTLA_HD uint32_t log_append(uint32_t l, uint32_t entry) {
+  uint32_t n = log_len(l);
+  return ((l & ~7u) | (n + 1)) | (entry << (3 + 5 * n));
+}
+RTLA_HD uint32_t log_prefix(uint32_t l, uint32_t n) {  // SubSeq(l, 1, n)
+  uint32_t keep = (3 + 5 * n) >= 32 ? 0xffffffffu : ((1u << (3 + 5 * n)) - 1u);
+  return (l & keep & ~7u) | n;
+}
+// Index of an in-model log in the allLogs universe (little-endian mixed radix).
+RTLA_HD int log_index(const Layout& L, uint32_t l) {
+  int n = (int)log_len(l), idx = 0, pw = 1, B = L.T * L.V;
+  for (int k = 1; k <= n; k++) {
+    int d = ((int)log_term(l, k) - 1) * L.V + (int)log_val(l, k);
+    idx += d * pw;
+    pw *= B;
+  }
+  return L.log_off[n] + idx;
+}
+RTLA_HD uint32_t log_from_index(const Layout& L, int idx) {
+  int n = 0;
+  while (n + 1 <= L.L && idx >= L.log_off[n + 1]) n++;
+  int r = idx - L.log_off[n], B = L.T * L.V;
+  uint32_t l = 0;
+  for (int k = 0; k < n; k++) {
+    int d = r % B;
+    r /= B;
+    uint32_t t = (uint32_t)(d / L.V + 1), v = (uint32_t)(d % L.V);
+    l = log_append(l, t | v << 3);
+  }
+  return l;
+}
+
+// Messages
+RTLA_HD uint32_t m_type(uint64_t k) { return (uint32_t)(k & 3u); }
+RTLA_HD uint32_t m_src(uint64_t k) { return (uint32_t)(k >> 2) & 7u; }
+RTLA_HD uint32_t m_dst(uint64_t k) { return (uint32_t)(k >> 5) & 7u; }
+RTLA_HD uint32_t m_term(uint64_t k) { return (uint32_t)(k >> 8) & 15u; }
+RTLA_HD uint32_t m_count(uint64_t v) { return (uint32_t)(v >> 60); }
+RTLA_HD uint64_t m_key(uint64_t v) { return v & ((1ull << 60) - 1); }
+RTLA_HD uint64_t m_base(uint32_t type, uint32_t src, uint32_t dst, uint32_t term) {
+  return (uint64_t)type | (uint64_t)src << 2 | (uint64_t)dst << 5 | (uint64_t)term << 8;
+}
+RTLA_HD uint64_t m_rvreq(uint32_t src, uint32_t dst, uint32_t term, uint32_t llt, uint32_t lli) {
+  return m_base(RVREQ, src, dst, term) | (uint64_t)llt << 12 | (uint64_t)lli << 16;
+}
+RTLA_HD uint64_t m_rvresp(uint32_t src, uint32_t dst, uint32_t term, uint32_t granted, uint32_t mlog) {
+  return m_base(RVRESP, src, dst, term) | (uint64_t)granted << 12 | (uint64_t)mlog << 16;
+}
+RTLA_HD uint64_t m_aereq(uint32_t src, uint32_t dst, uint32_t term, uint32_t prev, uint32_t prevt,
+                         uint32_t has, uint32_t entry, uint32_t commit, uint32_t mlog) {
+  return m_base(AEREQ, src, dst, term) | (uint64_t)prev << 12 | (uint64_t)prevt << 15 |
+         (uint64_t)has << 19 | (uint64_t)entry << 20 | (uint64_t)commit << 25 | (uint64_t)mlog << 28;
+}
+RTLA_HD uint64_t m_aeresp(uint32_t src, uint32_t dst, uint32_t term, uint32_t success, uint32_t match) {
+  return m_base(AERESP, src, dst, term) | (uint64_t)success << 12 | (uint64_t)match << 13;
+}
+RTLA_HD uint32_t m_f(uint64_t k, int lo, int bits) { return (uint32_t)(k >> lo) & ((1u << bits) - 1u); }
+
+// --------------------------------------------------------------- hash ----
+struct FP {
+  uint64_t a, b;
+};
+RTLA_HD uint64_t mix_a(uint64_t z) {  // splitmix64 finalizer
+  z ^= z >> 30; z *= 0xbf58476d1ce4e5b9ull;
+  z ^= z >> 27; z *= 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return z;
+}
+RTLA_HD uint64_t mix_b(uint64_t z) {  // murmur3 fmix64 (independent constants)
+  z ^= z >> 33; z *= 0xff51afd7ed558ccdull;
+  z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ull;
+  z ^= z >> 33;
+  return z;
+}
+RTLA_HD FP fp_add(FP x, FP y) { return FP{x.a + y.a, x.b + y.b}; }
+RTLA_HD FP fp_sub(FP x, FP y) { return FP{x.a - y.a, x.b - y.b}; }
+RTLA_HD FP hash_u64(uint64_t tag, uint64_t x) {
+  FP h;
+  h.a = mix_a(mix_a(tag * 0x9E3779B97F4A7C15ull + 0x243f6a8885a308d3ull) ^ x);
+  h.b = mix_b(mix_b(tag * 0xD1B54A32D192ED03ull + 0x13198a2e03707344ull) + x);
+  return h;
+}
+template <class P>
+RTLA_HD FP hash_words(uint64_t tag, P w, int n) {
+  uint64_t a = mix_a(tag * 0x9E3779B97F4A7C15ull + 0x243f6a8885a308d3ull);
+  uint64_t b = mix_b(tag * 0xD1B54A32D192ED03ull + 0x13198a2e03707344ull);
+  for (int k = 0; k < n; k += 2) {
+    uint64_t x = (uint64_t)w[k] | ((k + 1 < n) ? (uint64_t)w[k + 1] << 32 : 0ull);
+    a = mix_a(a ^ x);
+    b = mix_b(b + x);
+  }
+  return FP{a, b};
+}
+enum { TAG_SRV = 1, TAG_MSG = 2, TAG_ALL = 3, TAG_ELEC = 4 };
+RTLA_HD FP h_srv(int i, const uint32_t* rec, int SW) { return hash_words((uint64_t)(TAG_SRV << 8 | i), rec, SW); }
+RTLA_HD FP h_msg(uint64_t slot) { return slot ? hash_u64(TAG_MSG, slot) : FP{0, 0}; }
+RTLA_HD FP h_all(int idx) { return hash_u64(TAG_ALL, (uint64_t)idx); }
+RTLA_HD FP h_elec(const uint32_t* rec, int EW) { return hash_words(TAG_ELEC, rec, EW); }
+
+// ------------------------------------------------------------ row I/O ----
+template <class P>
+RTLA_HD uint64_t bag_slot(const Layout& L, P row, int k) {
+  return (uint64_t)row[L.off_bag + 2 * k] | (uint64_t)row[L.off_bag + 2 * k + 1] << 32;
+}
+template <class P>
+RTLA_HD int row_nmsg(const Layout& L, P row) { return (int)(row[L.off_hdr] & 255u); }
+template <class P>
+RTLA_HD int row_nelec(const Layout& L, P row) { return (int)((row[L.off_hdr] >> 8) & 255u); }
+template <class P>
+RTLA_HD FP row_fp(P row) {
+  return FP{(uint64_t)row[0] | (uint64_t)row[1] << 32, (uint64_t)row[2] | (uint64_t)row[3] << 32};
+}
+template <class P>
+RTLA_HD void row_set_fp(P row, FP f) {
+  row[0] = (uint32_t)f.a; row[1] = (uint32_t)(f.a >> 32);
+  row[2] = (uint32_t)f.b; row[3] = (uint32_t)(f.b >> 32);
+}
+
+// Full fingerprint of a row, from scratch (Init, checks).
+template <class P>
+RTLA_HD FP row_fingerprint(const Layout& L, P row) {
+  FP f{0, 0};
+  uint32_t rec[3 + NMAX];
+  for (int i = 0; i < L.N; i++) {
+    for (int w = 0; w < L.SW; w++) rec[w] = row[L.off_srv + i * L.SW + w];
+    f = fp_add(f, h_srv(i, rec, L.SW));
+  }
+  int nm = row_nmsg(L, row);
+  for (int k = 0; k < nm; k++) f = fp_add(f, h_msg(bag_slot(L, row, k)));
+  for (int x = 0; x < L.n_logs; x++)
+    if (row[L.off_all + (x >> 5)] >> (x & 31) & 1u) f = fp_add(f, h_all(x));
+  int ne = row_nelec(L, row);
+  uint32_t er[2 + NMAX];
+  for (int e = 0; e < ne; e++) {
+    for (int w = 0; w < L.EW; w++) er[w] = row[L.off_elec + e * L.EW + w];
+    f = fp_add(f, h_elec(er, L.EW));
+  }
+  return f;
+}
+
+// Init (raft.tla:140-160): exactly one state.
+template <class P>
+RTLA_HD void row_init(const Layout& L, P row) {
+  for (int w = 0; w < L.W; w++) row[w] = 0;
+  for (int i = 0; i < L.N; i++) {
+    uint32_t* r = nullptr;
+    (void)r;
+    row[L.off_srv + i * L.SW + 0] = s_make(1, FOLLOWER, NIL, 0, 0, 0, 0);  // :143-147
+    row[L.off_srv + i * L.SW + 1] = 0;                                     // log = <<>> :153
+    row[L.off_srv + i * L.SW + 2] = nm_fill(L.N, 1, 0);                    // :151-152
+  }
+  row_set_fp(row, row_fingerprint(L, row));
+}
+
+// --------------------------------------------------------------- delta ----
+// The successor of one action instance, as a patch of the parent row.
+struct Delta {
+  int32_t enabled;
+  int32_t in_model;
+  int32_t sub;             // Receive sub-action (R_*) or R_NONE
+  int32_t err;             // 1: spec evaluation error, 2: row capacity overflow
+  int32_t srv;             // server whose record changes, -1 = none
+  uint32_t rec[3 + NMAX];  // its new record
+  int32_t nops;            // bag slot writes
+  int32_t op_slot[3];
+  uint64_t op_old[3], op_new[3];
+  int32_t nmsg;            // new number of bag slots in use
+  int32_t elec;            // 1: append erec to elections
+  uint32_t erec[2 + NMAX];
+};
+
+template <class P>
+RTLA_HD uint64_t bag_get(const Layout& L, P row, const Delta& d, int slot) {
+  for (int q = 0; q < d.nops; q++)
+    if (d.op_slot[q] == slot) return d.op_new[q];
+  return bag_slot(L, row, slot);
+}
+template <class P>
+RTLA_HD void bag_set(const Layout& L, P row, Delta& d, int slot, uint64_t v) {
+  for (int q = 0; q < d.nops; q++)
+    if (d.op_slot[q] == slot) { d.op_new[q] = v; return; }
+  if (d.nops >= 3) { d.err = 2; return; }
+  d.op_slot[d.nops] = slot;
+  d.op_old[d.nops] = bag_slot(L, row, slot);
+  d.op_new[d.nops] = v;
+  d.nops++;
+}
+template <class P>
+RTLA_HD int bag_find(const Layout& L, P row, const Delta& d, uint64_t key) {
+  for (int k = 0; k < d.nmsg; k++)
+    if (m_key(bag_get(L, row, d, k)) == key) return k;
+  return -1;
+}
+// raft.tla:106-110 WithMessage
+template <class P>
+RTLA_HD void with_message(const Layout& L, P row, Delta& d, uint64_t key) {
+  int p = bag_find(L, row, d, key);
+  if (p >= 0) {
+    bag_set(L, row, d, p, bag_get(L, row, d, p) + (1ull << 60));
+  } else {
+    if (d.nmsg >= L.K) { d.err = 2; return; }
+    bag_set(L, row, d, d.nmsg, key | (1ull << 60));
+    d.nmsg++;
+  }
+}
+// raft.tla:114-119 WithoutMessage
+template <class P>
+RTLA_HD void without_message(const Layout& L, P row, Delta& d, uint64_t key) {
+  int p = bag_find(L, row, d, key);
+  if (p < 0) return;
+  uint64_t v = bag_get(L, row, d, p);
+  if (m_count(v) <= 1) {
+    int last = d.nmsg - 1;
+    if (p != last) bag_set(L, row, d, p, bag_get(L, row, d, last));
+    bag_set(L, row, d, last, 0);
+    d.nmsg--;
+  } else {
+    bag_set(L, row, d, p, v - (1ull << 60));
+  }
+}
+
+template <class P>
+RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
+  for (int w = 0; w < L.SW; w++) rec[w] = row[L.off_srv + i * L.SW + w];
+}
+
+// Compute the successor of `row` under action instance `inst` (0..L.fam[F_COUNT]).
+// Follows raft.tla:454-463; allLogs' (:465) is applied per parent by the caller.
+template <class P>
+RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
+  const int N = L.N;
+  d.enabled = 0; d.in_model = 1; d.sub = R_NONE; d.err = 0; d.srv = -1; d.nops = 0;
+  d.nmsg = row_nmsg(L, row); d.elec = 0;
+  int fam = 0;
+  while (fam + 1 < F_COUNT && inst >= L.fam[fam + 1]) fam++;
+  int x = inst - L.fam[fam];
+  uint32_t* rec = d.rec;
+
+  if (fam == F_RESTART) {                       // Restart(i) :167-175
+    int i = x;
+    load_rec(L, row, i, rec);
+    rec[0] = s_make(s_term(rec[0]), FOLLOWER, s_voted(rec[0]), 0, 0, 0, 0);
+    rec[2] = nm_fill(N, 1, 0);
+    for (int j = 0; j < N; j++) rec[3 + j] = 0;
+    d.srv = i; d.enabled = 1;
+  } else if (fam == F_TIMEOUT) {                // Timeout(i) :178-187
+    int i = x;
+    load_rec(L, row, i, rec);
+    uint32_t role = s_role(rec[0]);
+    if (role != FOLLOWER && role != CANDIDATE) return;
+    uint32_t t = s_term(rec[0]) + 1;
+    rec[0] = s_make(t, CANDIDATE, NIL, s_commit(rec[0]), 0, 0, 0);
+    for (int j = 0; j < N; j++) rec[3 + j] = 0;
+    d.srv = i; d.enabled = 1;
+    if ((int)t > L.T) d.in_model = 0;
+  } else if (fam == F_REQUESTVOTE) {            // RequestVote(i, j) :190-199
+    int i = x / N, j = x % N;
+    uint32_t w0 = row[L.off_srv + i * L.SW], lg = row[L.off_srv + i * L.SW + 1];
+    if (s_role(w0) != CANDIDATE || (s_vresp(w0) >> j & 1u)) return;
+    with_message(L, row, d, m_rvreq(i, j, s_term(w0), last_term(lg), log_len(lg)));
+    d.enabled = 1;
+  } else if (fam == F_BECOMELEADER) {           // BecomeLeader(i) :229-243
+    int i = x;
+    load_rec(L, row, i, rec);
+    uint32_t w0 = rec[0];
+    if (s_role(w0) != CANDIDATE) return;
+    if (!(__builtin_popcount(s_vgrant(w0)) * 2 > N)) return;   // votesGranted[i] \in Quorum :99
+    d.enabled = 1; d.srv = i;
+    rec[0] = (w0 & ~(3u << 4)) | (LEADER << 4);
+    rec[2] = nm_fill(N, log_len(rec[1]) + 1, 0);
+    // elections' = elections \cup {[eterm, eleader, elog, evotes, evoterLog]}
+    d.erec[0] = s_term(w0) | (uint32_t)i << 4 | s_vgrant(w0) << 7 | s_vlp(w0) << 12;
+    d.erec[1] = rec[1];
+    for (int j = 0; j < N; j++) d.erec[2 + j] = row[L.off_srv + i * L.SW + 3 + j];
+    int ne = row_nelec(L, row), dup = 0;
+    for (int e = 0; e < ne; e++) {
+      int same = 1;
+      for (int w = 0; w < L.EW; w++) same &= row[L.off_elec + e * L.EW + w] == d.erec[w];
+      dup |= same;
+    }
+    if (!dup) {
+      if (ne >= L.E) { d.err = 2; return; }
+      d.elec = 1;
+    }
+  } else if (fam == F_CLIENTREQUEST) {          // ClientRequest(i, v) :246-253
+    int i = x / L.V, v = x % L.V;
+    load_rec(L, row, i, rec);
+    if (s_role(rec[0]) != LEADER) return;
+    if (log_len(rec[1]) >= (uint32_t)LMAX + 1) { d.err = 2; return; }
+    rec[1] = log_append(rec[1], s_term(rec[0]) | (uint32_t)v << 3);
+    d.srv = i; d.enabled = 1;
+    if ((int)log_len(rec[1]) > L.L) d.in_model = 0;
+  } else if (fam == F_ADVANCECOMMIT) {          // AdvanceCommitIndex(i) :259-276
+    int i = x;
+    load_rec(L, row, i, rec);
+    if (s_role(rec[0]) != LEADER) return;
+    int len = (int)log_len(rec[1]), maxagree = 0;
+    for (int index = 1; index <= len; index++) {
+      int agree = 1;                            // Agree(index) = {i} \cup {k : matchIndex[i][k] >= index}
+      for (int k = 0; k < N; k++) agree += (k != i) && (int)nm_match(rec[2], k) >= index;
+      if (agree * 2 > N) maxagree = index;
+    }
+    uint32_t nci = s_commit(rec[0]);
+    if (maxagree > 0 && log_term(rec[1], maxagree) == s_term(rec[0])) nci = (uint32_t)maxagree;
+    rec[0] = (rec[0] & ~(7u << 9)) | nci << 9;
+    d.srv = i; d.enabled = 1;
+  } else if (fam == F_APPENDENTRIES) {          // AppendEntries(i, j) :204-226
+    int i = x / N, j = x % N;
+    if (i == j) return;
+    uint32_t w0 = row[L.off_srv + i * L.SW], lg = row[L.off_srv + i * L.SW + 1];
+    uint32_t nm = row[L.off_srv + i * L.SW + 2];
+    if (s_role(w0) != LEADER) return;
+    uint32_t nxt = nm_next(nm, j), prev = nxt - 1, len = log_len(lg);
+    uint32_t prevt = 0;
+    if (prev > 0) {
+      if (prev > len) { d.err = 1; return; }   // log[i][prevLogIndex] outside DOMAIN
+      prevt = log_term(lg, prev);
+    }
+    uint32_t last = len < nxt ? len : nxt;    // Min({Len(log[i]), nextIndex[i][j]})
+    uint32_t has = nxt <= last ? 1u : 0u;      // SubSeq(log[i], next, lastEntry)
+    uint32_t entry = has ? log_entry(lg, nxt) : 0u;
+    uint32_t ci = s_commit(w0);
+    uint32_t mci = ci < last ? ci : last;
+    with_message(L, row, d, m_aereq(i, j, s_term(w0), prev, prevt, has, entry, mci, lg));
+    d.enabled = 1;
+  } else if (fam == F_RECEIVE) {                // Receive(m) :421-436
+    if (x >= d.nmsg) return;
+    uint64_t key = m_key(bag_slot(L, row, x));
+    int i = (int)m_dst(key), j = (int)m_src(key);
+    uint32_t mt = m_term(key), type = m_type(key);
+    load_rec(L, row, i, rec);
+    uint32_t cur = s_term(rec[0]), role = s_role(rec[0]);
+    if (mt > cur) {                              // UpdateTerm :406-412 (message kept)
+      rec[0] = s_make(mt, FOLLOWER, NIL, s_commit(rec[0]), s_vresp(rec[0]), s_vgrant(rec[0]), s_vlp(rec[0]));
+      d.srv = i; d.enabled = 1; d.sub = R_UPDATETERM;
+      return;
+    }
+    uint32_t lg = rec[1], len = log_len(lg);
+    if (type == RVREQ) {                         // HandleRequestVoteRequest :284-303
+      uint32_t llt = m_f(key, 12, 4), lli = m_f(key, 16, 3), lt = last_term(lg);
+      int logok = llt > lt || (llt == lt && lli >= len);
+      uint32_t vf = s_voted(rec[0]);
+      int grant = mt == cur && logok && (vf == NIL || vf == (uint32_t)j);
+      if (grant) {
+        rec[0] = (rec[0] & ~(7u << 6)) | (uint32_t)j << 6;
+        d.srv = i;
+      }
+      with_message(L, row, d, m_rvresp(i, j, cur, grant ? 1u : 0u, lg));  // Reply :129-130
+      without_message(L, row, d, key);
+      d.enabled = 1; d.sub = R_HRVREQ;
+    } else if (type == RVRESP || type == AERESP) {
+      if (mt < cur) {                            // DropStaleResponse :415-418
+        without_message(L, row, d, key);
+        d.enabled = 1; d.sub = R_DROPSTALE;
+      } else if (type == RVRESP) {               // HandleRequestVoteResponse :307-321
+        uint32_t vr = s_vresp(rec[0]) | 1u << j, vg = s_vgrant(rec[0]), vlp = s_vlp(rec[0]);
+        if (m_f(key, 12, 1)) {
+          vg |= 1u << j;
+          if (!(vlp >> j & 1u)) {                // voterLog[i] @@ (j :> m.mlog): left wins
+            vlp |= 1u << j;
+            rec[3 + j] = m_f(key, 16, 28);
+          }
+        }
+        rec[0] = s_make(cur, role, s_voted(rec[0]), s_commit(rec[0]), vr, vg, vlp);
+        without_message(L, row, d, key);
+        d.srv = i; d.enabled = 1; d.sub = R_HRVRESP;
+      } else {                                   // HandleAppendEntriesResponse :393-403
+        uint32_t succ = m_f(key, 12, 1), mm = m_f(key, 13, 3);
+        if (succ) {
+          rec[2] = nm_set_match(nm_set_next(rec[2], j, mm + 1), j, mm);
+        } else {
+          uint32_t nx = nm_next(rec[2], j);
+          rec[2] = nm_set_next(rec[2], j, nx > 2 ? nx - 1 : 1);   // Max({next - 1, 1})
+        }
+        without_message(L, row, d, key);
+        d.srv = i; d.enabled = 1; d.sub = R_HAERESP;
+      }
+    } else {                                     // HandleAppendEntriesRequest :327-389
+      uint32_t prev = m_f(key, 12, 3), prevt = m_f(key, 15, 4), has = m_f(key, 19, 1);
+      uint32_t entry = m_f(key, 20, 5), mci = m_f(key, 25, 3);
+      int logok = prev == 0 || (prev > 0 && prev <= len && prevt == log_term(lg, prev));
+      if (mt < cur || (mt == cur && role == FOLLOWER && !logok)) {   // reject :333-345
+        with_message(L, row, d, m_aeresp(i, j, cur, 0, 0));
+        without_message(L, row, d, key);
+        d.enabled = 1; d.sub = R_HAEREQ;
+      } else if (mt == cur && role == CANDIDATE) {                  // return to follower :346-350
+        rec[0] = (rec[0] & ~(3u << 4)) | (FOLLOWER << 4);
+        d.srv = i; d.enabled = 1; d.sub = R_HAEREQ;
+      } else if (mt == cur && role == FOLLOWER && logok) {          // accept :351-388
+        uint32_t index = prev + 1;
+        if (!has || (len >= index && log_term(lg, index) == (entry & 7u))) {  // already done :356-374
+          rec[0] = (rec[0] & ~(7u << 9)) | mci << 9;
+          d.srv = i;
+          with_message(L, row, d, m_aeresp(i, j, cur, 1, prev + has));
+          without_message(L, row, d, key);
+          d.enabled = 1; d.sub = R_HAEREQ;
+        } else if (len >= index) {               // conflict: remove 1 entry :375-382
+          rec[1] = log_prefix(lg, len - 1);
+          d.srv = i; d.enabled = 1; d.sub = R_HAEREQ;
+        } else if (len == prev) {                // no conflict: append entry :383-388
+          rec[1] = log_append(lg, entry);
+          d.srv = i; d.enabled = 1; d.sub = R_HAEREQ;
+        }
+      }
+      // AEReq with mterm = currentTerm at a Leader: no disjunct enabled.
+    }
+  } else if (fam == F_DUPLICATE) {              // DuplicateMessage(m) :443-445
+    if (x >= d.nmsg) return;
+    bag_set(L, row, d, x, bag_slot(L, row, x) + (1ull << 60));
+    d.enabled = 1;
+  } else {                                      // DropMessage(m) :448-450
+    if (x >= d.nmsg) return;
+    without_message(L, row, d, m_key(bag_slot(L, row, x)));
+    d.enabled = 1;
+  }
+  if (!d.enabled) return;
+  // State constraint (oracle/MC.tla) on the changed components.
+  if (d.srv >= 0) {
+    if ((int)s_term(d.rec[0]) > L.T || (int)log_len(d.rec[1]) > L.L) d.in_model = 0;
+  }
+  if (d.nops) {
+    int total_delta = 0;
+    for (int q = 0; q < d.nops; q++) {
+      if ((int)m_count(d.op_new[q]) > L.C) d.in_model = 0;
+      total_delta += (int)m_count(d.op_new[q]) - (int)m_count(d.op_old[q]);
+    }
+    if (L.M > 0 && total_delta > 0) {
+      int total = 0;
+      int nm = row_nmsg(L, row);
+      for (int k = 0; k < nm; k++) total += (int)m_count(bag_slot(L, row, k));
+      if (total + total_delta > L.M) d.in_model = 0;
+    }
+  }
+}
+
+// Fingerprint change of the delta (allLogs change excluded: per parent).
+template <class P>
+RTLA_HD FP delta_fp(const Layout& L, P row, const Delta& d) {
+  FP f{0, 0};
+  if (d.srv >= 0) {
+    uint32_t old[3 + NMAX];
+    load_rec(L, row, d.srv, old);
+    f = fp_sub(h_srv(d.srv, d.rec, L.SW), h_srv(d.srv, old, L.SW));
+  }
+  for (int q = 0; q < d.nops; q++) f = fp_add(f, fp_sub(h_msg(d.op_new[q]), h_msg(d.op_old[q])));
+  if (d.elec) f = fp_add(f, h_elec(d.erec, L.EW));
+  return f;
+}
+
+// allLogs' = allLogs \cup {log[i] : i \in Server}   (pre-state logs, raft.tla:465)
+// Writes the new allLogs words into all_out and returns the fingerprint change.
+template <class P, class Q>
+RTLA_HD FP alllogs_delta(const Layout& L, P row, Q all_out) {
+  FP f{0, 0};
+  for (int w = 0; w < L.all_words; w++) all_out[w] = row[L.off_all + w];
+  for (int i = 0; i < L.N; i++) {
+    int x = log_index(L, row[L.off_srv + i * L.SW + 1]);
+    uint32_t bit = 1u << (x & 31);
+    if (!(all_out[x >> 5] & bit)) {
+      all_out[x >> 5] |= bit;
+      f = fp_add(f, h_all(x));
+    }
+  }
+  return f;
+}
+
+// Materialise the successor row: child = parent + delta, with new allLogs
+// words and fingerprint.  `child` may alias nothing in `row`.
+template <class P, class Q, class R>
+RTLA_HD void materialize(const Layout& L, P row, const Delta& d, R all_new, FP fp, Q child) {
+  for (int w = 0; w < L.W; w++) child[w] = row[w];
+  row_set_fp(child, fp);
+  int ne = row_nelec(L, row) + (d.elec ? 1 : 0);
+  child[L.off_hdr] = (uint32_t)d.nmsg | (uint32_t)ne << 8;
+  if (d.srv >= 0)
+    for (int w = 0; w < L.SW; w++) child[L.off_srv + d.srv * L.SW + w] = d.rec[w];
+  for (int w = 0; w < L.all_words; w++) child[L.off_all + w] = all_new[w];
+  if (d.elec)
+    for (int w = 0; w < L.EW; w++) child[L.off_elec + (ne - 1) * L.EW + w] = d.erec[w];
+  for (int q = 0; q < d.nops; q++) {
+    child[L.off_bag + 2 * d.op_slot[q]] = (uint32_t)d.op_new[q];
+    child[L.off_bag + 2 * d.op_slot[q] + 1] = (uint32_t)(d.op_new[q] >> 32);
+  }
+}
+
+// ---------------------------------------------------------- invariants ----
+// Evaluated on the successor (parent + delta) without materialising it.
+// Returns the mask of VIOLATED invariants among L.inv_mask.
+template <class P>
+RTLA_HD int check_invariants(const Layout& L, P row, const Delta* d) {
+  const int N = L.N;
+  int bad = 0;
+  uint32_t w0[NMAX], lg[NMAX];
+  for (int i = 0; i < N; i++) {
+    w0[i] = row[L.off_srv + i * L.SW];
+    lg[i] = row[L.off_srv + i * L.SW + 1];
+  }
+  if (d && d->srv >= 0) { w0[d->srv] = d->rec[0]; lg[d->srv] = d->rec[1]; }
+  if (L.inv_mask & INV_NO_TWO_LEADERS) {
+    // NoTwoLeaders == \A i, j \in Server : state[i] = Leader /\ state[j] = Leader => i = j
+    int nl = 0;
+    for (int i = 0; i < N; i++) nl += s_role(w0[i]) == LEADER;
+    if (nl > 1) bad |= INV_NO_TWO_LEADERS;
+  }
+  if (L.inv_mask & INV_ELECTION_SAFETY) {
+    // ElectionSafety == \A e, f \in elections : e.eterm = f.eterm => e.eleader = f.eleader
+    int ne = row_nelec(L, row);
+    int tot = ne + ((d && d->elec) ? 1 : 0);
+    for (int a = 0; a < tot; a++) {
+      uint32_t ea = a < ne ? row[L.off_elec + a * L.EW] : d->erec[0];
+      for (int b = a + 1; b < tot; b++) {
+        uint32_t eb = b < ne ? row[L.off_elec + b * L.EW] : d->erec[0];
+        if ((ea & 15u) == (eb & 15u) && ((ea >> 4) & 7u) != ((eb >> 4) & 7u)) bad |= INV_ELECTION_SAFETY;
+      }
+    }
+  }
+  if (L.inv_mask & INV_LOG_MATCHING) {
+    // LogMatching == \A i, j \in Server : \A n \in 1..Min({Len(log[i]), Len(log[j])}) :
+    //   log[i][n].term = log[j][n].term => SubSeq(log[i],1,n) = SubSeq(log[j],1,n)
+    for (int i = 0; i < N; i++)
+      for (int j = i + 1; j < N; j++) {
+        uint32_t a = lg[i], b = lg[j];
+        uint32_t m = log_len(a) < log_len(b) ? log_len(a) : log_len(b);
+        for (uint32_t n = 1; n <= m; n++)
+          if (log_term(a, n) == log_term(b, n) && log_prefix(a, n) != log_prefix(b, n))
+            bad |= INV_LOG_MATCHING;
+      }
+  }
+  return bad;
+}
+
+}  // namespace rtla

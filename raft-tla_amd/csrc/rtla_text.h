@@ -1,0 +1,17 @@
+// rtla_text.h -- decode packed rows into TLC-style value text.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+
+#include "rtla_model.h"
+
+namespace rtla {
+
+// Canonical TLC-like text of a state: "/\ var = value" lines in the variable
+// declaration order of raft.tla:32-85, sets and bag domains sorted by text.
+std::string state_text(const Layout& L, const uint32_t* row);
+// Human-readable label of an action instance (+ Receive sub-action).
+std::string action_name(const Layout& L, int inst, int sub);
+
+}  // namespace rtla

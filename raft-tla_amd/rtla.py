@@ -1,0 +1,347 @@
+"""Python host-side mirror of the C ABI (include/rtla.h) over ctypes.
+
+This is the user-facing API of the MI355X model checker for Python callers
+(tests, bench.py).  It mirrors TLC's model-checking contract for
+/root/reference/raft.tla + a raft.cfg-style model (raft.cfg:1-15):
+
+    res = rtla.check(rtla.Config(n_server=3, n_value=1, max_term=2, max_log=1,
+                                 max_copies=1, max_msgs=2,
+                                 invariants=("NoTwoLeaders",)))
+    res.distinct, res.generated, res.depth, res.violation, res.trace
+
+There is no CPU fallback: every entry point runs the HIP kernels in
+librtla.so, and importing this module raises if the library is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtla.so")
+
+OK, DONE, VIOLATION = 0, 1, 2
+INV_BITS = {"NoTwoLeaders": 1, "ElectionSafety": 2, "LogMatching": 4}
+COVER_NAMES = ["Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
+               "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
+               "DropMessage", "UpdateTerm", "HandleRequestVoteRequest",
+               "HandleRequestVoteResponse", "HandleAppendEntriesRequest",
+               "HandleAppendEntriesResponse", "DropStaleResponse"]
+
+
+class RtlaError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = _lib.rtla_strerror(status).decode() if _lib else str(status)
+        super().__init__("%s: %s (status %d)" % (what, msg, status))
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("n_server", C.c_int32), ("n_value", C.c_int32), ("max_term", C.c_int32),
+                ("max_log", C.c_int32), ("max_copies", C.c_int32), ("max_msgs", C.c_int32),
+                ("bag_cap", C.c_int32), ("elec_cap", C.c_int32), ("inv_mask", C.c_int32),
+                ("symmetry", C.c_int32), ("fpset_log2", C.c_int32), ("reserved", C.c_int32),
+                ("frontier_cap", C.c_uint64), ("mem_budget", C.c_uint64)]
+
+
+class _Stats(C.Structure):
+    _fields_ = [("level", C.c_int32), ("status", C.c_int32), ("frontier", C.c_uint64),
+                ("new_states", C.c_uint64), ("generated", C.c_uint64),
+                ("distinct_total", C.c_uint64), ("generated_total", C.c_uint64),
+                ("seconds", C.c_double), ("kernel_ms", C.c_double), ("probes", C.c_uint64),
+                ("row_bytes", C.c_uint64)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("librtla.so not built at %s (run `make -C raft-tla_amd` or "
+                          "__graft_entry__.build())" % LIB_PATH)
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    sig = {
+        "rtla_open": (C.c_int, [P(_Cfg), C.c_int, C.c_int, C.c_void_p, P(C.c_void_p)]),
+        "rtla_close": (None, [C.c_void_p]),
+        "rtla_init": (C.c_int, [C.c_void_p, P(_Stats)]),
+        "rtla_step": (C.c_int, [C.c_void_p, P(_Stats)]),
+        "rtla_reset": (C.c_int, [C.c_void_p]),
+        "rtla_violation": (C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
+        "rtla_trace": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_int32), C.c_size_t, P(C.c_size_t)]),
+        "rtla_frontier": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
+        "rtla_coverage": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int]),
+        "rtla_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+        "rtla_row_words": (C.c_int, [P(_Cfg)]),
+        "rtla_init_row": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
+        "rtla_expand_batch": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, P(C.c_uint32),
+                                        P(C.c_uint64), C.c_size_t, P(C.c_size_t)]),
+        "rtla_state_text": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_char_p, C.c_size_t]),
+        "rtla_action_name": (C.c_int, [P(_Cfg), C.c_int32, C.c_int32, C.c_char_p, C.c_size_t]),
+        "rtla_invariants": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
+        "rtla_strerror": (C.c_char_p, [C.c_int]),
+        "rtla_abi_version": (C.c_int, []),
+        "rtla_comm_id": (C.c_int, [C.c_void_p]),
+        "rtla_probe_bench": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_uint64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = _load()
+
+EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset", "rtla_step", "rtla_violation",
+            "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
+            "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants",
+            "rtla_strerror", "rtla_abi_version", "rtla_probe_bench"]
+
+
+@dataclass(frozen=True)
+class Config:
+    """A raft.cfg-style model: constants + the build's StateConstraint bounds."""
+    n_server: int = 3
+    n_value: int = 1
+    max_term: int = 2
+    max_log: int = 1
+    max_copies: int = 1
+    max_msgs: int = 0
+    invariants: Tuple[str, ...] = ("NoTwoLeaders",)
+    bag_cap: int = 0
+    elec_cap: int = 0
+    fpset_log2: int = 0
+    frontier_cap: int = 0
+    mem_budget: int = 0
+
+    @property
+    def inv_mask(self) -> int:
+        m = 0
+        for n in self.invariants:
+            m |= INV_BITS[n]
+        return m
+
+    def c(self) -> _Cfg:
+        return _Cfg(self.n_server, self.n_value, self.max_term, self.max_log, self.max_copies,
+                    self.max_msgs, self.bag_cap, self.elec_cap, self.inv_mask, 0,
+                    self.fpset_log2, 0, self.frontier_cap, self.mem_budget)
+
+
+@dataclass
+class Level:
+    level: int
+    frontier: int
+    new: int
+    generated: int
+    seconds: float
+    kernel_ms: float = 0.0
+    probes: int = 0
+    row_bytes: int = 0
+
+
+@dataclass
+class Result:
+    distinct: int = 0
+    generated: int = 0
+    depth: int = 0
+    levels: List[Level] = field(default_factory=list)
+    violation: Optional[str] = None
+    violation_in_model: bool = True
+    trace: Optional[List[Tuple[str, str]]] = None   # (action label, state text)
+    coverage: Optional[dict] = None
+    seconds: float = 0.0
+
+
+def _check(st: int, what: str):
+    if st < 0:
+        raise RtlaError(st, what)
+    return st
+
+
+def row_words(cfg: Config) -> int:
+    cc = cfg.c()
+    return _check(_lib.rtla_row_words(C.byref(cc)), "rtla_row_words")
+
+
+def init_row(cfg: Config):
+    cc = cfg.c()
+    w = row_words(cfg)
+    buf = (C.c_uint32 * w)()
+    _check(_lib.rtla_init_row(C.byref(cc), buf), "rtla_init_row")
+    return list(buf)
+
+
+def state_text(cfg: Config, row: Sequence[int]) -> str:
+    cc = cfg.c()
+    arr = (C.c_uint32 * len(row))(*row)
+    cap = 1 << 16
+    while True:
+        buf = C.create_string_buffer(cap)
+        st = _lib.rtla_state_text(C.byref(cc), arr, buf, cap)
+        if st >= 0:
+            return buf.value.decode()
+        cap *= 4
+        if cap > 1 << 26:
+            raise RtlaError(st, "rtla_state_text")
+
+
+def action_name(cfg: Config, inst: int, sub: int) -> str:
+    cc = cfg.c()
+    buf = C.create_string_buffer(256)
+    _check(_lib.rtla_action_name(C.byref(cc), inst, sub, buf, 256), "rtla_action_name")
+    return buf.value.decode()
+
+
+def invariants_violated(cfg: Config, row: Sequence[int]) -> int:
+    cc = cfg.c()
+    arr = (C.c_uint32 * len(row))(*row)
+    return _check(_lib.rtla_invariants(C.byref(cc), arr), "rtla_invariants")
+
+
+def expand_batch(cfg: Config, rows: Sequence[Sequence[int]]):
+    """GPU successor generation (TLC getNextStates) for a batch of rows.
+
+    Returns a list of (input index, instance, receive-sub, in_model, row),
+    sorted by (input, instance)."""
+    cc = cfg.c()
+    w = row_words(cfg)
+    n = len(rows)
+    flat = (C.c_uint32 * (max(n, 1) * w))()
+    for k, r in enumerate(rows):
+        assert len(r) == w, "row width mismatch"
+        flat[k * w:(k + 1) * w] = list(r)
+    cap = max(n, 1) * 512
+    succ = (C.c_uint32 * (cap * w))()
+    info = (C.c_uint64 * cap)()
+    nout = C.c_size_t(0)
+    _check(_lib.rtla_expand_batch(C.byref(cc), flat, n, succ, info, cap, C.byref(nout)),
+           "rtla_expand_batch")
+    out = []
+    for k in range(nout.value):
+        v = info[k]
+        out.append((v >> 32, v & 0xFFFF, (v >> 16) & 0x7FFF, bool(v >> 31 & 1),
+                    list(succ[k * w:(k + 1) * w])))
+    return out
+
+
+class Checker:
+    """One BFS context on one GPU (rank)."""
+
+    def __init__(self, cfg: Config, rank: int = 0, world: int = 1, comm_id: bytes = None):
+        self.cfg = cfg
+        self._cc = cfg.c()
+        h = C.c_void_p()
+        cid = C.create_string_buffer(comm_id, 128) if comm_id else None
+        _check(_lib.rtla_open(C.byref(self._cc), rank, world, cid, C.byref(h)), "rtla_open")
+        self._h = h
+        self.levels: List[Level] = []
+        self.status = OK
+
+    def close(self):
+        if self._h:
+            _lib.rtla_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def device_info(self) -> str:
+        buf = C.create_string_buffer(1024)
+        _check(_lib.rtla_device_info(self._h, buf, 1024), "rtla_device_info")
+        return buf.value.decode()
+
+    def _rec(self, st: _Stats):
+        self.levels.append(Level(st.level, st.frontier, st.new_states, st.generated, st.seconds,
+                                 st.kernel_ms, st.probes, st.row_bytes))
+        self.distinct, self.generated = st.distinct_total, st.generated_total
+
+    def init(self) -> int:
+        st = _Stats()
+        self.status = _check(_lib.rtla_init(self._h, C.byref(st)), "rtla_init")
+        self._rec(st)
+        return self.status
+
+    def reset(self):
+        _check(_lib.rtla_reset(self._h), "rtla_reset")
+        self.levels = []
+        self.status = OK
+
+    def step(self) -> int:
+        st = _Stats()
+        self.status = _check(_lib.rtla_step(self._h, C.byref(st)), "rtla_step")
+        self._rec(st)
+        return self.status
+
+    def run(self, max_levels: int = 100000) -> int:
+        if not self.levels:
+            if self.init() != OK:
+                return self.status
+        while self.status == OK and len(self.levels) < max_levels:
+            self.step()
+        return self.status
+
+    def violation(self):
+        m, im = C.c_int32(0), C.c_int32(0)
+        _lib.rtla_violation(self._h, C.byref(m), C.byref(im))
+        names = [n for n, b in INV_BITS.items() if m.value & b]
+        return (names[0] if names else None), bool(im.value)
+
+    def trace(self) -> List[Tuple[str, str]]:
+        w = row_words(self.cfg)
+        n = C.c_size_t(0)
+        _lib.rtla_trace(self._h, None, None, 0, C.byref(n))
+        cap = n.value
+        rows = (C.c_uint32 * (cap * w))()
+        labels = (C.c_int32 * cap)()
+        _check(_lib.rtla_trace(self._h, rows, labels, cap, C.byref(n)), "rtla_trace")
+        out = []
+        for k in range(n.value):
+            lab = labels[k]
+            name = "Initial predicate" if lab < 0 else action_name(self.cfg, lab & 0xFFFF, (lab >> 16) & 0x7FFF)
+            out.append((name, state_text(self.cfg, list(rows[k * w:(k + 1) * w]))))
+        return out
+
+    def frontier(self):
+        """Rows of the level last produced (debug / parity)."""
+        w = row_words(self.cfg)
+        n = C.c_size_t(0)
+        _check(_lib.rtla_frontier(self._h, None, 0, C.byref(n)), "rtla_frontier")
+        buf = (C.c_uint32 * max(1, n.value * w))()
+        _check(_lib.rtla_frontier(self._h, buf, n.value, C.byref(n)), "rtla_frontier")
+        return [list(buf[k * w:(k + 1) * w]) for k in range(n.value)]
+
+    def coverage(self) -> dict:
+        n = len(COVER_NAMES)
+        g, d = (C.c_uint64 * n)(), (C.c_uint64 * n)()
+        _check(_lib.rtla_coverage(self._h, g, d, n), "rtla_coverage")
+        return {COVER_NAMES[k]: (g[k], d[k]) for k in range(n)}
+
+
+def check(cfg: Config, trace: bool = True) -> Result:
+    """Exhaustive BFS of the model (TLC `-workers N` breadth-first mode)."""
+    with Checker(cfg) as ck:
+        st = ck.run()
+        res = Result(distinct=ck.distinct, generated=ck.generated, levels=list(ck.levels))
+        res.depth = sum(1 for lv in ck.levels if lv.new > 0)
+        res.seconds = sum(lv.seconds for lv in ck.levels)
+        res.coverage = ck.coverage()
+        if st == VIOLATION:
+            res.violation, res.violation_in_model = ck.violation()
+            if trace:
+                res.trace = ck.trace()
+        return res
+
+
+def probe_bench(log2: int, n: int):
+    s, ins = C.c_double(0), C.c_uint64(0)
+    _check(_lib.rtla_probe_bench(log2, n, C.byref(s), C.byref(ins)), "rtla_probe_bench")
+    return s.value, ins.value

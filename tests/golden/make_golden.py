@@ -1,0 +1,70 @@
+"""Generate the golden BFS fixtures in tests/golden/bfs_counts.json.
+
+Each case is run through the C oracle (oracle/raft_cpu.c); cases marked
+"py" are also run through the value-semantics oracle (oracle/raft_values.py)
+and the two must agree on every level's counts and state-text hash before the
+case is written.  The configs are the build's bounded models (specs/MC.tla);
+the reference ships no fixtures of its own.
+
+    python tests/golden/make_golden.py [--big]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import raft_cpu  # noqa: E402
+import raft_values as rv  # noqa: E402
+
+NTL, ES, LM = "NoTwoLeaders", "ElectionSafety", "LogMatching"
+# name: (N, V, T, L, C, M, invariants, py, big)
+CASES = {
+    "n1_v1_t2_l1": (1, 1, 2, 1, 1, 0, (NTL,), True, False),
+    "n1_v2_t3_l2": (1, 2, 3, 2, 1, 0, (NTL, ES, LM), True, False),
+    "n2_v1_t2_l1_m1": (2, 1, 2, 1, 1, 1, (NTL,), True, False),
+    "n2_v1_t3_l1_m1": (2, 1, 3, 1, 1, 1, (NTL, ES, LM), True, False),
+    "n2_v1_t2_l1_c2_m2": (2, 1, 2, 1, 2, 2, (NTL,), False, False),
+    "n2_v2_t3_l2_m1": (2, 2, 3, 2, 1, 1, (ES, LM), False, False),
+    "n3_v1_t3_l1_m1_ntl": (3, 1, 3, 1, 1, 1, (NTL,), False, False),
+    "n3_v1_t2_l1_m1": (3, 1, 2, 1, 1, 1, (NTL,), False, False),
+    "n2_v1_t2_l1": (2, 1, 2, 1, 1, 0, (NTL,), False, True),
+    "n3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, (NTL,), False, True),
+    "n3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, (ES, LM), False, True),
+}
+
+
+def main():
+    big = "--big" in sys.argv
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bfs_counts.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    raft_cpu.build()
+    for name, (n, v, t, l, c, m, inv, py, is_big) in CASES.items():
+        if is_big and not big:
+            continue
+        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big, text_hash=not is_big)
+        assert r["rc"] >= 0, (name, r["rc"])
+        case = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c,
+                "max_msgs": m, "invariants": list(inv), "distinct": r["distinct"],
+                "generated": r["generated"], "depth": r["depth"], "levels": r["levels"],
+                "violated": r["violated"], "trace_len": r["trace_len"], "source": "oracle/raft_cpu.c"}
+        if not is_big:
+            case["level_text_hash"] = ["%016x" % h for h in r["level_text_hash"]]
+        if py:
+            pc = rv.Cfg(n, v, t, l, c, inv, m)
+            pr = rv.bfs(pc)
+            assert [list(x) for x in pr.levels] == r["levels"], name
+            assert (pr.violation is not None) == bool(r["violated"]), name
+            if not r["violated"]:
+                ph = rv.level_text_hashes(pc)
+                assert ph == r["level_text_hash"][:len(ph)], name
+            case["source"] += " + oracle/raft_values.py"
+        out[name] = case
+        print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
