@@ -75,9 +75,12 @@ typedef struct {
     int32_t inv_mask;    /* RTLA_INV_* */
     int32_t symmetry;    /* must be 0 in this version */
     int32_t fpset_log2;  /* log2(#8-byte slots) of this rank's fingerprint set; 0 = auto */
-    int32_t reserved;
+    int32_t shards;      /* world == 1 only: split the search on this GPU into this many
+                            fingerprint-owned shards (same exchange protocol as multi-GPU,
+                            transport = device copies); 0/1 = one shard */
     uint64_t frontier_cap; /* states per frontier buffer; 0 = auto */
     uint64_t mem_budget;   /* bytes of HBM this context may use; 0 = 85% of free */
+    uint64_t chunk;        /* multi-shard: frontier states expanded per exchange round; 0 = auto */
 } rtla_cfg;
 
 typedef struct {

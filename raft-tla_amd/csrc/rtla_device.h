@@ -16,6 +16,24 @@ enum {
   FLAG_ROW_OVERFLOW = 2,    // bag / elections capacity of the row format exceeded
   FLAG_FRONTIER_FULL = 4,   // next-frontier buffer too small
   FLAG_FPSET_FULL = 8,      // fingerprint set probe limit hit
+  FLAG_OUTBOX_FULL = 16,    // exchange outbox region too small
+};
+
+// Fingerprint ownership across shards (ranks): low 32 bits of fp.a scaled to
+// [0, nshard).  The fingerprint-set home slot uses the TOP bits of fp.a, so
+// ownership and placement are independent.
+RTLA_HD int fp_owner(FP f, int nshard) {
+  return (int)(((f.a & 0xffffffffull) * (unsigned long long)nshard) >> 32);
+}
+
+// Outbox of one shard for one expansion chunk: region p (capacity `cap`
+// records) holds the successors owned by shard p.
+struct ShardBox {
+  int nshard, me;
+  unsigned long long cap;
+  unsigned long long* out_count;  // [nshard]
+  unsigned long long* send_fp;    // [nshard][cap][2]
+  unsigned long long* send_ref;   // [nshard][cap]: local parent index << 16 | instance
 };
 
 // Per-level device counters (zeroed before each level except `cover`).

@@ -1,14 +1,36 @@
 // rtla_host.cpp -- the C-ABI driver (include/rtla.h) around the HIP kernels.
 //
-// One context = one rank = one GPU.  Device memory per context:
+// A context owns one or more SHARDS.  A shard is the unit of fingerprint
+// ownership: it holds the part of the fingerprint set whose fingerprints it
+// owns (fp_owner, rtla_device.h), the states it materialised (frontier double
+// buffer) and their parent pointers.  Device memory per shard:
 //   fingerprint set   2^fpset_log2 x 8 B   (open addressing, CAS insert)
-//   parents           one u64 per distinct state: parent global index << 16 | instance
+//   parents           one u64 per state: parent shard-local index << 16 | instance
 //   frontier A / B    frontier_cap rows each (double buffer, swapped per level)
-//   counters          DevCounters
-// The level loop is host-driven: one k_expand launch per BFS level, then an
-// 8-byte-scale counter read-back decides termination (TLC's "0 states left on
-// queue").
+//   outbox / inbox    (multi-shard only) per destination: fingerprints, refs, answers
+//
+// Deployments:
+//   world == 1, shards <= 1 : the whole search in one shard; one fused k_expand
+//                             launch per BFS level (expand + probe + insert +
+//                             materialise + invariants).
+//   world == N (one process per GPU, RCCL over xGMI): one shard per rank.
+//   world == 1, shards == S : S shards on one GPU, exchanging by device copies
+//                             -- the multi-GPU protocol exercised on one device.
+//
+// Multi-shard level (per chunk of the frontier, all shards in lock-step):
+//   1. k_expand: successors owned locally are probed/inserted/materialised at
+//      once; the others are queued as (fp, parent, instance) per owner;
+//   2. all-gather of the per-destination counts, then all-to-all-v of the
+//      16-byte fingerprints (ncclSend/ncclRecv pairs in one group: all 7 xGMI
+//      links of an MI355X node carry traffic at once);
+//   3. k_insert_remote at the owner answers new/seen (1 byte per record);
+//   4. all-to-all-v of the answers back;
+//   5. k_materialize at the sender builds the winners next to their parents,
+//      so traces never cross shards.
+// Then one all-reduce of {new, generated, probes, violation, flags} decides
+// termination (TLC's "0 states left on queue").
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
@@ -25,38 +47,71 @@
 
 using namespace rtla;
 
-struct rtla_ctx {
-  rtla_cfg cfg;
-  Layout L;
-  int rank = 0, world = 1, device = 0;
-  hipStream_t stream = nullptr;
+namespace {
+
+struct Shard {
+  int id = 0;
   uint64_t* table = nullptr;
-  int tlog2 = 0;
   uint64_t* parents = nullptr;
   uint64_t parents_cap = 0;
   uint32_t* front[2] = {nullptr, nullptr};
-  uint64_t front_cap = 0;
   int cur = 0;
   uint64_t n_cur = 0, cur_base = 0;
   DevCounters* ctr = nullptr;
   int* dflags = nullptr;
+  // exchange buffers (nshard > 1)
+  uint64_t* out_count = nullptr;   // [G] device: records queued per destination
+  uint64_t* in_count = nullptr;    // [G] device: records received per source
+  uint64_t* all_count = nullptr;   // [G][G] device (RCCL all-gather target)
+  uint64_t* send_fp = nullptr;     // [G][cap][2]
+  uint64_t* send_ref = nullptr;    // [G][cap]
+  uint8_t* send_res = nullptr;     // [G][cap]
+  uint64_t* recv_fp = nullptr;     // [G][cap][2]
+  uint8_t* recv_res = nullptr;     // [G][cap]
+  std::vector<uint64_t> h_out, h_in;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // violation found on this shard
+  int viol_mask = 0, viol_in_model = 0, viol_inst = -1;
+  uint64_t viol_parent = 0, viol_child = ~0ull;
+};
+
+}  // namespace
+
+struct rtla_ctx {
+  rtla_cfg cfg;
+  Layout L;
+  int rank = 0, world = 1, device = 0;
+  int nshard = 1;          // shards in the whole job
+  int shard0 = 0;          // global id of sh[0]
+  std::vector<Shard> sh;   // shards held by this process
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  int tlog2 = 0;
+  uint64_t front_cap = 0, box_cap = 0, chunk = 0;
+  uint64_t* red = nullptr;  // device scratch for all-reduces
   int level = 0;
   bool inited = false, finished = false;
   uint64_t distinct = 0, generated = 0;
-  int viol_mask = 0, viol_in_model = 0, viol_inst = -1;
-  uint64_t viol_parent = 0, viol_child = ~0ull;
   int grid = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<uint32_t> init_row;
 };
 
-#define HIPCHK(x)                                                     \
-  do {                                                                \
-    hipError_t e_ = (x);                                              \
-    if (e_ != hipSuccess) {                                           \
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) {                                                                         \
       fprintf(stderr, "rtla: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
-      return RTLA_E_HIP;                                              \
-    }                                                                 \
+      return RTLA_E_HIP;                                                                            \
+    }                                                                                               \
+  } while (0)
+
+#define NCCLCHK(x)                                                                                    \
+  do {                                                                                                \
+    ncclResult_t r_ = (x);                                                                            \
+    if (r_ != ncclSuccess) {                                                                          \
+      fprintf(stderr, "rtla: RCCL error %s at %s:%d\n", ncclGetErrorString(r_), __FILE__, __LINE__); \
+      return RTLA_E_COMM;                                                                             \
+    }                                                                                                 \
   } while (0)
 
 static int layout_from_cfg(const rtla_cfg* c, Layout* L) {
@@ -65,8 +120,8 @@ static int layout_from_cfg(const rtla_cfg* c, Layout* L) {
   int K = c->bag_cap ? c->bag_cap : (c->max_msgs > 0 ? c->max_msgs + 1 : 32);
   int E = c->elec_cap ? c->elec_cap : (c->max_term - 1) * c->n_server;
   if (E < 1) E = 1;
-  if (make_layout(L, c->n_server, c->n_value, c->max_term, c->max_log, c->max_copies, c->max_msgs,
-                  K, E, c->inv_mask) != 0)
+  if (make_layout(L, c->n_server, c->n_value, c->max_term, c->max_log, c->max_copies, c->max_msgs, K, E,
+                  c->inv_mask) != 0)
     return RTLA_E_CONFIG;
   return RTLA_OK;
 }
@@ -80,7 +135,7 @@ extern "C" const char* rtla_strerror(int s) {
     case RTLA_VIOLATION: return "invariant violated";
     case RTLA_E_CONFIG: return "configuration outside the supported row format";
     case RTLA_E_HIP: return "HIP runtime error";
-    case RTLA_E_OVERFLOW: return "capacity overflow (bag/elections/frontier/fingerprint set)";
+    case RTLA_E_OVERFLOW: return "capacity overflow (bag/elections/frontier/fingerprint set/outbox)";
     case RTLA_E_SPEC: return "TLC evaluation error in Next (index outside DOMAIN)";
     case RTLA_E_STATE: return "call out of order";
     case RTLA_E_ARG: return "bad argument";
@@ -141,9 +196,10 @@ static void report_flags(int flags) {
   if (flags & FLAG_ROW_OVERFLOW) fprintf(stderr, "rtla: row capacity exceeded (raise bag_cap / elec_cap)\n");
   if (flags & FLAG_FRONTIER_FULL) fprintf(stderr, "rtla: next-frontier buffer full (raise frontier_cap / mem_budget)\n");
   if (flags & FLAG_FPSET_FULL) fprintf(stderr, "rtla: fingerprint set too full (raise fpset_log2)\n");
+  if (flags & FLAG_OUTBOX_FULL) fprintf(stderr, "rtla: exchange outbox full (lower chunk)\n");
 }
 
-// Run k_expand_batch on device rows; results copied to host vectors.
+// Run k_expand_batch on device rows; results copied to host, sorted by (input, instance).
 static int expand_batch_dev(const Layout& L, const uint32_t* d_rows, size_t n, std::vector<uint32_t>& out,
                             std::vector<uint64_t>& info, hipStream_t st) {
   size_t cap = n * (size_t)L.fam[F_COUNT];
@@ -167,8 +223,9 @@ static int expand_batch_dev(const Layout& L, const uint32_t* d_rows, size_t n, s
     HIPCHK(hipMemcpy(out.data(), d_out, m * L.W * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(info.data(), d_info, m * 8, hipMemcpyDeviceToHost));
   }
-  hipFree(d_out); hipFree(d_info); hipFree(d_ctr);
-  // canonical order: (input, instance)
+  (void)hipFree(d_out);
+  (void)hipFree(d_info);
+  (void)hipFree(d_ctr);
   std::vector<size_t> ord(m);
   for (size_t k = 0; k < m; k++) ord[k] = k;
   std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
@@ -186,8 +243,8 @@ static int expand_batch_dev(const Layout& L, const uint32_t* d_rows, size_t n, s
   return rc;
 }
 
-extern "C" int rtla_expand_batch(const rtla_cfg* c, const uint32_t* rows, size_t n, uint32_t* succ,
-                                 uint64_t* info, size_t cap, size_t* n_out) {
+extern "C" int rtla_expand_batch(const rtla_cfg* c, const uint32_t* rows, size_t n, uint32_t* succ, uint64_t* info,
+                                 size_t cap, size_t* n_out) {
   Layout L;
   int r = layout_from_cfg(c, &L);
   if (r) return r;
@@ -198,7 +255,7 @@ extern "C" int rtla_expand_batch(const rtla_cfg* c, const uint32_t* rows, size_t
   std::vector<uint32_t> out;
   std::vector<uint64_t> inf;
   r = expand_batch_dev(L, d_rows, n, out, inf, nullptr);
-  hipFree(d_rows);
+  (void)hipFree(d_rows);
   if (r < 0) return r;
   *n_out = inf.size();
   if (inf.size() > cap) return RTLA_E_ARG;
@@ -208,95 +265,180 @@ extern "C" int rtla_expand_batch(const rtla_cfg* c, const uint32_t* rows, size_t
 }
 
 extern "C" int rtla_comm_id(void* out128) {
-  (void)out128;
-  return RTLA_E_COMM;  // multi-rank contexts: see rtla_dist.cpp (not in this build)
+  if (!out128) return RTLA_E_ARG;
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+  memcpy(out128, &id, 128);
+  return RTLA_OK;
+}
+
+static void free_shard(Shard& s) {
+  void* ptrs[] = {s.table, s.parents, s.front[0], s.front[1], s.ctr, s.dflags, s.out_count, s.in_count,
+                  s.all_count, s.send_fp, s.send_ref, s.send_res, s.recv_fp, s.recv_res};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (s.ev0) (void)hipEventDestroy(s.ev0);
+  if (s.ev1) (void)hipEventDestroy(s.ev1);
+  s = Shard();
+}
+
+extern "C" void rtla_close(rtla_ctx* x) {
+  if (!x) return;
+  (void)hipSetDevice(x->device);
+  for (auto& s : x->sh) free_shard(s);
+  if (x->red) (void)hipFree(x->red);
+  if (x->comm) ncclCommDestroy(x->comm);
+  if (x->stream) (void)hipStreamDestroy(x->stream);
+  delete x;
+}
+
+static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
+  const Layout& L = x->L;
+  const int G = x->nshard;
+  uint64_t tbytes = 8ull << x->tlog2;
+  s.parents_cap = (1ull << x->tlog2) - (1ull << x->tlog2) / 4;  // load factor <= 0.75
+  uint64_t pbytes = s.parents_cap * 8;
+  uint64_t rowb = (uint64_t)L.W * 4;
+  uint64_t boxb = G > 1 ? (uint64_t)G * x->box_cap * (16 + 8 + 1 + 16 + 1) : 0;
+  if (!x->front_cap) {
+    uint64_t used = tbytes + pbytes + boxb;
+    uint64_t rest = budget > used ? budget - used : 0;
+    x->front_cap = std::max<uint64_t>(rest / (2 * rowb), 1024);
+  }
+  HIPCHK(hipMalloc(&s.table, tbytes));
+  HIPCHK(hipMalloc(&s.parents, pbytes));
+  HIPCHK(hipMalloc(&s.front[0], x->front_cap * rowb));
+  HIPCHK(hipMalloc(&s.front[1], x->front_cap * rowb));
+  HIPCHK(hipMalloc(&s.ctr, sizeof(DevCounters)));
+  HIPCHK(hipMalloc(&s.dflags, sizeof(int) * 64));
+  if (G > 1) {
+    HIPCHK(hipMalloc(&s.out_count, 8 * G));
+    HIPCHK(hipMalloc(&s.in_count, 8 * G));
+    HIPCHK(hipMalloc(&s.all_count, 8 * G * G));
+    HIPCHK(hipMalloc(&s.send_fp, 16 * G * x->box_cap));
+    HIPCHK(hipMalloc(&s.send_ref, 8 * G * x->box_cap));
+    HIPCHK(hipMalloc(&s.send_res, G * x->box_cap));
+    HIPCHK(hipMalloc(&s.recv_fp, 16 * G * x->box_cap));
+    HIPCHK(hipMalloc(&s.recv_res, G * x->box_cap));
+    s.h_out.assign(G, 0);
+    s.h_in.assign(G, 0);
+  }
+  HIPCHK(hipMemsetAsync(s.table, 0, tbytes, x->stream));
+  HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
+  HIPCHK(hipEventCreate(&s.ev0));
+  HIPCHK(hipEventCreate(&s.ev1));
+  return RTLA_OK;
 }
 
 extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* comm_id, rtla_ctx** out) {
-  (void)comm_id;
-  if (!cfg || !out) return RTLA_E_ARG;
+  if (!cfg || !out || world < 1 || rank < 0 || rank >= world) return RTLA_E_ARG;
   *out = nullptr;
-  if (world != 1) return RTLA_E_CONFIG;
+  if (world > 1 && !comm_id) return RTLA_E_ARG;
+  if (world > 1 && cfg->shards > 1) return RTLA_E_CONFIG;
   rtla_ctx* x = new rtla_ctx();
   x->cfg = *cfg;
   int r = layout_from_cfg(cfg, &x->L);
   if (r) { delete x; return r; }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) { delete x; return RTLA_E_HIP; }
-  x->rank = rank; x->world = world; x->device = rank % ndev;
+  x->rank = rank;
+  x->world = world;
+  x->device = rank % ndev;
+  x->nshard = world > 1 ? world : std::max(1, cfg->shards);
+  x->shard0 = world > 1 ? rank : 0;
+  int nlocal = world > 1 ? 1 : x->nshard;
   if (hipSetDevice(x->device) != hipSuccess) { delete x; return RTLA_E_HIP; }
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) { delete x; return RTLA_E_HIP; }
+  if (world > 1) {
+    ncclUniqueId id;
+    memcpy(&id, comm_id, sizeof id);
+    if (ncclCommInitRank(&x->comm, world, id, rank) != ncclSuccess) { rtla_close(x); return RTLA_E_COMM; }
+  }
   size_t free_b = 0, total_b = 0;
-  hipMemGetInfo(&free_b, &total_b);
+  (void)hipMemGetInfo(&free_b, &total_b);
   uint64_t budget = cfg->mem_budget ? cfg->mem_budget : (uint64_t)(free_b * 0.85);
+  uint64_t per = budget / nlocal;
   const Layout& L = x->L;
-  // fingerprint set: <= 40% of the budget, power of two
+  const int G = x->nshard;
+  // exchange sizing: one frontier state queues at most (fixed + 3 * bag_cap)
+  // records, all possibly for the same destination
+  if (G > 1) {
+    uint64_t nmax = (uint64_t)(L.fam[F_RECEIVE] + 3 * L.K);
+    x->chunk = cfg->chunk;
+    if (!x->chunk) {
+      x->chunk = (per / 8) / ((uint64_t)G * nmax * 42);
+      x->chunk = std::min<uint64_t>(std::max<uint64_t>(x->chunk, 1024), 1u << 20);
+    }
+    x->box_cap = x->chunk * nmax;
+  }
   int tl = cfg->fpset_log2;
   if (!tl) {
     tl = 20;
-    while (tl < 34 && (8ull << (tl + 1)) <= budget * 2 / 5) tl++;
+    while (tl < 34 && (8ull << (tl + 1)) <= per * 2 / 5) tl++;
   }
   if (tl < 10 || tl > 40) { rtla_close(x); return RTLA_E_CONFIG; }
   x->tlog2 = tl;
-  uint64_t tbytes = 8ull << tl;
-  x->parents_cap = (1ull << tl) - (1ull << tl) / 4;  // load factor <= 0.75
-  uint64_t pbytes = x->parents_cap * 8;
-  uint64_t rowb = (uint64_t)L.W * 4;
-  uint64_t fcap = cfg->frontier_cap;
-  if (!fcap) {
-    uint64_t rest = budget > tbytes + pbytes ? budget - tbytes - pbytes : 0;
-    fcap = rest / (2 * rowb);
+  x->front_cap = cfg->frontier_cap;
+  x->sh.resize(nlocal);
+  for (int k = 0; k < nlocal; k++) {
+    x->sh[k].id = x->shard0 + k;
+    if (alloc_shard(x, x->sh[k], per) != RTLA_OK) {
+      fprintf(stderr, "rtla: device allocation failed (fpset 2^%d slots, frontier 2x%llu rows of %d B)\n", tl,
+              (unsigned long long)x->front_cap, L.W * 4);
+      rtla_close(x);
+      return RTLA_E_HIP;
+    }
   }
-  if (fcap < 1024) fcap = 1024;
-  x->front_cap = fcap;
-  if (hipMalloc(&x->table, tbytes) != hipSuccess || hipMalloc(&x->parents, pbytes) != hipSuccess ||
-      hipMalloc(&x->front[0], fcap * rowb) != hipSuccess || hipMalloc(&x->front[1], fcap * rowb) != hipSuccess ||
-      hipMalloc(&x->ctr, sizeof(DevCounters)) != hipSuccess || hipMalloc(&x->dflags, sizeof(int) * 64) != hipSuccess) {
-    fprintf(stderr, "rtla: device allocation failed (table %llu B, parents %llu B, frontier 2x%llu B)\n",
-            (unsigned long long)tbytes, (unsigned long long)pbytes, (unsigned long long)(fcap * rowb));
+  if (hipMalloc(&x->red, 64 * 8) != hipSuccess || hipStreamSynchronize(x->stream) != hipSuccess) {
     rtla_close(x);
     return RTLA_E_HIP;
   }
-  hipMemsetAsync(x->table, 0, tbytes, x->stream);
-  hipMemsetAsync(x->ctr, 0, sizeof(DevCounters), x->stream);
-  if (hipStreamSynchronize(x->stream) != hipSuccess) { rtla_close(x); return RTLA_E_HIP; }
   hipDeviceProp_t prop;
-  hipGetDeviceProperties(&prop, x->device);
+  (void)hipGetDeviceProperties(&prop, x->device);
   x->grid = prop.multiProcessorCount * expand_blocks_per_cu(L) * 2;
-  hipEventCreate(&x->ev0);
-  hipEventCreate(&x->ev1);
   *out = x;
   return RTLA_OK;
-}
-
-extern "C" void rtla_close(rtla_ctx* x) {
-  if (!x) return;
-  hipSetDevice(x->device);
-  if (x->table) hipFree(x->table);
-  if (x->parents) hipFree(x->parents);
-  if (x->front[0]) hipFree(x->front[0]);
-  if (x->front[1]) hipFree(x->front[1]);
-  if (x->ctr) hipFree(x->ctr);
-  if (x->dflags) hipFree(x->dflags);
-  if (x->ev0) hipEventDestroy(x->ev0);
-  if (x->ev1) hipEventDestroy(x->ev1);
-  if (x->stream) hipStreamDestroy(x->stream);
-  delete x;
 }
 
 extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
   if (!x || !buf) return RTLA_E_ARG;
   hipDeviceProp_t p;
   HIPCHK(hipGetDeviceProperties(&p, x->device));
-  snprintf(buf, cap, "{\"device\": \"%s\", \"arch\": \"%s\", \"cus\": %d, \"fpset_slots_log2\": %d, "
-           "\"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d}",
-           p.name, p.gcnArchName, p.multiProcessorCount, x->tlog2, (unsigned long long)x->front_cap,
-           x->L.W, x->grid);
+  snprintf(buf, cap,
+           "{\"device\": \"%s\", \"arch\": \"%s\", \"cus\": %d, \"rank\": %d, \"world\": %d, \"shards\": %d, "
+           "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu}",
+           p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
+           (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk);
   return RTLA_OK;
 }
 
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Sum (op 0) or max (op 1) of n u64 over all ranks; host in/out.
+static int allreduce_u64(rtla_ctx* x, uint64_t* v, int n, int op) {
+  if (x->world == 1) return RTLA_OK;
+  HIPCHK(hipMemcpyAsync(x->red, v, 8 * n, hipMemcpyHostToDevice, x->stream));
+  NCCLCHK(ncclAllReduce(x->red, x->red, n, ncclUint64, op ? ncclMax : ncclSum, x->comm, x->stream));
+  HIPCHK(hipMemcpyAsync(v, x->red, 8 * n, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return RTLA_OK;
+}
+
+extern "C" int rtla_reset(rtla_ctx* x) {
+  if (!x) return RTLA_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  for (auto& s : x->sh) {
+    HIPCHK(hipMemsetAsync(s.table, 0, 8ull << x->tlog2, x->stream));
+    HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
+    s.n_cur = 0; s.cur_base = 0; s.cur = 0;
+    s.viol_mask = 0; s.viol_in_model = 0; s.viol_inst = -1; s.viol_parent = 0; s.viol_child = ~0ull;
+  }
+  HIPCHK(hipStreamSynchronize(x->stream));
+  x->inited = false; x->finished = false; x->level = 0; x->distinct = 0; x->generated = 0;
+  return RTLA_OK;
 }
 
 extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
@@ -307,170 +449,319 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
   const Layout& L = x->L;
   x->init_row.assign(L.W, 0);
   row_init(L, x->init_row.data());
-  HIPCHK(hipMemcpyAsync(x->front[0], x->init_row.data(), L.W * 4, hipMemcpyHostToDevice, x->stream));
-  HIPCHK(launch_insert_rows(L, x->front[0], 1, x->table, x->tlog2, x->dflags, x->ctr, x->stream));
-  uint64_t root = ~0ull;  // Init has no parent
-  HIPCHK(hipMemcpyAsync(x->parents, &root, 8, hipMemcpyHostToDevice, x->stream));
+  // Init belongs to the shard that owns its fingerprint (raft.tla:155-160: one state)
+  int owner = fp_owner(row_fp(x->init_row.data()), x->nshard);
+  for (auto& s : x->sh) {
+    s.cur = 0; s.cur_base = 0; s.n_cur = 0;
+    if (s.id != owner) continue;
+    HIPCHK(hipMemcpyAsync(s.front[0], x->init_row.data(), L.W * 4, hipMemcpyHostToDevice, x->stream));
+    HIPCHK(launch_insert_rows(L, s.front[0], 1, s.table, x->tlog2, s.dflags, s.ctr, x->stream));
+    uint64_t root = ~0ull;
+    HIPCHK(hipMemcpyAsync(s.parents, &root, 8, hipMemcpyHostToDevice, x->stream));
+    s.n_cur = 1;
+  }
   HIPCHK(hipStreamSynchronize(x->stream));
-  x->cur = 0; x->n_cur = 1; x->cur_base = 0;
   x->level = 1; x->distinct = 1; x->generated = 1; x->inited = true;
   int bad = check_invariants(L, x->init_row.data(), (const Delta*)nullptr);
   int status = RTLA_OK;
   if (bad) {
-    x->viol_mask = bad; x->viol_in_model = 1; x->viol_child = 0; x->viol_inst = -1;
+    for (auto& s : x->sh)
+      if (s.id == owner) { s.viol_mask = bad; s.viol_in_model = 1; s.viol_child = 0; s.viol_inst = -1; }
     x->finished = true;
     status = RTLA_VIOLATION;
   }
   if (st) {
     memset(st, 0, sizeof *st);
-    st->level = 1; st->status = status; st->frontier = 0; st->new_states = 1; st->generated = 1;
+    st->level = 1; st->status = status; st->new_states = 1; st->generated = 1;
     st->distinct_total = 1; st->generated_total = 1; st->seconds = now_s() - t0;
     st->row_bytes = (uint64_t)L.W * 4;
   }
   return status;
 }
 
-extern "C" int rtla_reset(rtla_ctx* x) {
-  if (!x) return RTLA_E_ARG;
-  HIPCHK(hipSetDevice(x->device));
-  HIPCHK(hipMemsetAsync(x->table, 0, 8ull << x->tlog2, x->stream));
-  HIPCHK(hipMemsetAsync(x->ctr, 0, sizeof(DevCounters), x->stream));
+// ---- multi-shard exchange (transport: device copies for local shards, RCCL across ranks)
+
+// After expand: every shard knows h_out[p] (records queued for shard p).
+// Fill h_in[p] (records shard p sent here) and move the fingerprints.
+static int exchange_fps(rtla_ctx* x) {
+  const int G = x->nshard;
+  const uint64_t cap = x->box_cap;
+  if (x->world == 1) {
+    for (auto& dst : x->sh)
+      for (auto& src : x->sh) {
+        uint64_t n = src.h_out[dst.id];
+        dst.h_in[src.id] = n;
+        if (n)
+          HIPCHK(hipMemcpyAsync(dst.recv_fp + 2 * (uint64_t)src.id * cap, src.send_fp + 2 * (uint64_t)dst.id * cap,
+                                16 * n, hipMemcpyDeviceToDevice, x->stream));
+      }
+    for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.in_count, s.h_in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
+    return RTLA_OK;
+  }
+  Shard& s = x->sh[0];
+  NCCLCHK(ncclAllGather(s.out_count, s.all_count, G, ncclUint64, x->comm, x->stream));
+  std::vector<uint64_t> all((size_t)G * G);
+  HIPCHK(hipMemcpyAsync(all.data(), s.all_count, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
-  x->inited = false; x->finished = false; x->level = 0; x->distinct = 0; x->generated = 0;
-  x->n_cur = 0; x->cur_base = 0; x->cur = 0;
-  x->viol_mask = 0; x->viol_in_model = 0; x->viol_inst = -1; x->viol_parent = 0; x->viol_child = ~0ull;
+  for (int p = 0; p < G; p++) s.h_in[p] = all[(size_t)p * G + s.id];
+  HIPCHK(hipMemcpyAsync(s.in_count, s.h_in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
+  NCCLCHK(ncclGroupStart());
+  for (int p = 0; p < G; p++) {
+    if (p == s.id) continue;
+    NCCLCHK(ncclSend(s.send_fp + 2 * (uint64_t)p * cap, 2 * s.h_out[p], ncclUint64, p, x->comm, x->stream));
+    NCCLCHK(ncclRecv(s.recv_fp + 2 * (uint64_t)p * cap, 2 * s.h_in[p], ncclUint64, p, x->comm, x->stream));
+  }
+  NCCLCHK(ncclGroupEnd());
+  return RTLA_OK;
+}
+
+// Owners answered in recv_res; route the answers back into send_res.
+static int exchange_answers(rtla_ctx* x) {
+  const int G = x->nshard;
+  const uint64_t cap = x->box_cap;
+  if (x->world == 1) {
+    for (auto& src : x->sh)
+      for (auto& dst : x->sh) {
+        uint64_t n = src.h_out[dst.id];
+        if (n)
+          HIPCHK(hipMemcpyAsync(src.send_res + (uint64_t)dst.id * cap, dst.recv_res + (uint64_t)src.id * cap, n,
+                                hipMemcpyDeviceToDevice, x->stream));
+      }
+    return RTLA_OK;
+  }
+  Shard& s = x->sh[0];
+  NCCLCHK(ncclGroupStart());
+  for (int p = 0; p < G; p++) {
+    if (p == s.id) continue;
+    NCCLCHK(ncclSend(s.recv_res + (uint64_t)p * cap, s.h_in[p], ncclUint8, p, x->comm, x->stream));
+    NCCLCHK(ncclRecv(s.send_res + (uint64_t)p * cap, s.h_out[p], ncclUint8, p, x->comm, x->stream));
+  }
+  NCCLCHK(ncclGroupEnd());
   return RTLA_OK;
 }
 
 extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   if (!x) return RTLA_E_ARG;
-  if (!x->inited) return RTLA_E_STATE;
-  if (x->finished) return x->viol_mask ? RTLA_VIOLATION : RTLA_DONE;
+  if (!x->inited || x->finished) return RTLA_E_STATE;
   double t0 = now_s();
   HIPCHK(hipSetDevice(x->device));
   const Layout& L = x->L;
-  HIPCHK(hipMemsetAsync(x->ctr, 0, offsetof(DevCounters, cover), x->stream));
-  uint64_t next_base = x->cur_base + x->n_cur;
-  uint64_t next_cap = x->front_cap;
-  if (next_base >= x->parents_cap) return RTLA_E_OVERFLOW;
-  if (next_cap > x->parents_cap - next_base) next_cap = x->parents_cap - next_base;
-  uint64_t blocks = (x->n_cur + 3) / 4;
-  int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
-  HIPCHK(hipEventRecord(x->ev0, x->stream));
-  HIPCHK(launch_expand(L, x->front[x->cur], x->n_cur, x->cur_base, x->front[x->cur ^ 1], x->parents,
-                       next_base, next_cap, x->table, x->tlog2, x->ctr, grid, x->stream));
-  HIPCHK(hipEventRecord(x->ev1, x->stream));
-  DevCounters h;
-  HIPCHK(hipMemcpyAsync(&h, x->ctr, sizeof h, hipMemcpyDeviceToHost, x->stream));
+  const int G = x->nshard;
+  std::vector<uint64_t> next_base(x->sh.size()), next_cap(x->sh.size());
+  for (size_t k = 0; k < x->sh.size(); k++) {
+    Shard& s = x->sh[k];
+    HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
+    next_base[k] = s.cur_base + s.n_cur;
+    if (next_base[k] >= s.parents_cap) return RTLA_E_OVERFLOW;
+    next_cap[k] = std::min<uint64_t>(x->front_cap, s.parents_cap - next_base[k]);
+  }
+  for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev0, x->stream));
+  if (G == 1) {
+    Shard& s = x->sh[0];
+    ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+    uint64_t blocks = (s.n_cur + 3) / 4;
+    int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
+    HIPCHK(launch_expand(L, s.front[s.cur], 0, s.n_cur, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[0],
+                         next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream));
+  } else {
+    // lock-step chunks over the frontier; every shard runs the same number
+    uint64_t mx = 0;
+    for (auto& s : x->sh) mx = std::max(mx, s.n_cur);
+    int rc = allreduce_u64(x, &mx, 1, 1);
+    if (rc) return rc;
+    uint64_t rounds = (mx + x->chunk - 1) / x->chunk;
+    for (uint64_t c = 0; c < rounds; c++) {
+      for (size_t k = 0; k < x->sh.size(); k++) {
+        Shard& s = x->sh[k];
+        uint64_t b = std::min<uint64_t>(c * x->chunk, s.n_cur), e = std::min<uint64_t>(b + x->chunk, s.n_cur);
+        HIPCHK(hipMemsetAsync(s.out_count, 0, 8 * G, x->stream));
+        ShardBox box{G, s.id, (unsigned long long)x->box_cap, (unsigned long long*)s.out_count,
+                     (unsigned long long*)s.send_fp, (unsigned long long*)s.send_ref};
+        uint64_t blocks = (e - b + 3) / 4;
+        int grid = (int)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), (uint64_t)x->grid);
+        HIPCHK(launch_expand(L, s.front[s.cur], b, e, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[k],
+                             next_cap[k], s.table, x->tlog2, s.ctr, box, grid, x->stream));
+        HIPCHK(hipMemcpyAsync(s.h_out.data(), s.out_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+      }
+      HIPCHK(hipStreamSynchronize(x->stream));
+      for (auto& s : x->sh)
+        for (int p = 0; p < G; p++)
+          if (s.h_out[p] > x->box_cap) {
+            report_flags(FLAG_OUTBOX_FULL);
+            x->finished = true;
+            return RTLA_E_OVERFLOW;
+          }
+      rc = exchange_fps(x);
+      if (rc) return rc;
+      for (auto& s : x->sh)
+        HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_res, s.ctr,
+                                    x->stream));
+      rc = exchange_answers(x);
+      if (rc) return rc;
+      for (size_t k = 0; k < x->sh.size(); k++) {
+        Shard& s = x->sh[k];
+        HIPCHK(launch_materialize(L, s.front[s.cur], s.cur_base, s.send_ref, s.send_res, s.out_count, G, x->box_cap,
+                                  s.front[s.cur ^ 1], s.parents, next_base[k], next_cap[k], s.ctr, x->stream));
+      }
+    }
+  }
+  for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev1, x->stream));
+  // gather counters
+  uint64_t sums[4] = {0, 0, 0, 0};  // new, generated, probes, frontier
+  uint64_t maxs[3] = {0, 0, 0};     // flags, violation, device time (us)
+  std::vector<DevCounters> hc(x->sh.size());
+  for (size_t k = 0; k < x->sh.size(); k++)
+    HIPCHK(hipMemcpyAsync(&hc[k], x->sh[k].ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
-  if (h.flags) { report_flags(h.flags); x->finished = true; return flags_to_status(h.flags); }
-  float kms = 0.f;
-  hipEventElapsedTime(&kms, x->ev0, x->ev1);
-  uint64_t nnew = h.next_count;
-  x->generated += h.generated;
+  for (size_t k = 0; k < x->sh.size(); k++) {
+    Shard& s = x->sh[k];
+    float kms = 0.f;
+    (void)hipEventElapsedTime(&kms, s.ev0, s.ev1);
+    sums[0] += hc[k].next_count; sums[1] += hc[k].generated; sums[2] += hc[k].probes; sums[3] += s.n_cur;
+    maxs[0] |= (uint64_t)hc[k].flags;
+    maxs[1] = std::max<uint64_t>(maxs[1], hc[k].viol_mask ? 1 : 0);
+    maxs[2] = std::max<uint64_t>(maxs[2], (uint64_t)(kms * 1000.0));
+    if (hc[k].viol_mask && !s.viol_mask) {
+      s.viol_mask = hc[k].viol_mask; s.viol_in_model = hc[k].viol_in_model; s.viol_inst = hc[k].viol_inst;
+      s.viol_parent = hc[k].viol_parent; s.viol_child = hc[k].viol_child;
+    }
+  }
+  int rc = allreduce_u64(x, sums, 4, 0);
+  if (rc) return rc;
+  rc = allreduce_u64(x, maxs, 3, 1);
+  if (rc) return rc;
+  if (maxs[0]) { report_flags((int)maxs[0]); x->finished = true; return flags_to_status((int)maxs[0]); }
+  uint64_t nnew = sums[0];
+  x->generated += sums[1];
   x->distinct += nnew;
   x->level++;
   int status = RTLA_OK;
-  if (h.viol_mask) {
-    x->viol_mask = h.viol_mask; x->viol_in_model = h.viol_in_model; x->viol_inst = h.viol_inst;
-    x->viol_parent = h.viol_parent; x->viol_child = h.viol_child;
+  if (maxs[1]) {
     x->finished = true;
     status = RTLA_VIOLATION;
   } else if (nnew == 0) {
     x->finished = true;
     status = RTLA_DONE;
   }
+  for (size_t k = 0; k < x->sh.size(); k++) {
+    Shard& s = x->sh[k];
+    s.cur_base = next_base[k];
+    s.n_cur = hc[k].next_count;
+    s.cur ^= 1;
+  }
   if (st) {
     memset(st, 0, sizeof *st);
-    st->level = x->level; st->status = status; st->frontier = x->n_cur; st->new_states = nnew;
-    st->generated = h.generated; st->distinct_total = x->distinct; st->generated_total = x->generated;
-    st->kernel_ms = kms; st->probes = h.probes; st->row_bytes = (uint64_t)L.W * 4;
+    st->level = x->level; st->status = status; st->frontier = sums[3]; st->new_states = nnew;
+    st->generated = sums[1]; st->distinct_total = x->distinct; st->generated_total = x->generated;
+    st->kernel_ms = maxs[2] / 1000.0; st->probes = sums[2]; st->row_bytes = (uint64_t)L.W * 4;
+    st->seconds = now_s() - t0;
   }
-  x->cur_base = next_base;
-  x->n_cur = nnew;
-  x->cur ^= 1;
-  if (st) st->seconds = now_s() - t0;
   return status;
+}
+
+static Shard* viol_shard(rtla_ctx* x) {
+  for (auto& s : x->sh)
+    if (s.viol_mask) return &s;
+  return nullptr;
 }
 
 extern "C" int rtla_violation(rtla_ctx* x, int32_t* inv_mask, int32_t* in_model) {
   if (!x) return RTLA_E_ARG;
-  if (inv_mask) *inv_mask = x->viol_mask;
-  if (in_model) *in_model = x->viol_in_model;
-  return x->viol_mask ? RTLA_VIOLATION : RTLA_OK;
+  Shard* s = viol_shard(x);
+  if (inv_mask) *inv_mask = s ? s->viol_mask : 0;
+  if (in_model) *in_model = s ? s->viol_in_model : 0;
+  return s ? RTLA_VIOLATION : RTLA_OK;
 }
 
 extern "C" int rtla_frontier(rtla_ctx* x, uint32_t* rows, size_t cap, size_t* n) {
   if (!x || !n) return RTLA_E_ARG;
   if (!x->inited) return RTLA_E_STATE;
-  *n = (size_t)x->n_cur;
+  size_t tot = 0;
+  for (auto& s : x->sh) tot += s.n_cur;
+  *n = tot;
   if (!rows) return RTLA_OK;
-  if (x->n_cur > cap) return RTLA_E_ARG;
+  if (tot > cap) return RTLA_E_ARG;
   HIPCHK(hipSetDevice(x->device));
-  HIPCHK(hipMemcpy(rows, x->front[x->cur], (size_t)x->n_cur * x->L.W * 4, hipMemcpyDeviceToHost));
+  size_t off = 0;
+  for (auto& s : x->sh) {
+    if (s.n_cur)
+      HIPCHK(hipMemcpy(rows + off * x->L.W, s.front[s.cur], (size_t)s.n_cur * x->L.W * 4, hipMemcpyDeviceToHost));
+    off += s.n_cur;
+  }
   return RTLA_OK;
 }
 
 extern "C" int rtla_coverage(rtla_ctx* x, uint64_t* gen, uint64_t* distinct, int n) {
   if (!x) return RTLA_E_ARG;
-  DevCounters h;
   HIPCHK(hipSetDevice(x->device));
-  HIPCHK(hipMemcpy(&h, x->ctr, sizeof h, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> acc(2 * COVER_CODES, 0);
+  for (auto& s : x->sh) {
+    DevCounters h;
+    HIPCHK(hipMemcpy(&h, s.ctr, sizeof h, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 2 * COVER_CODES; k++) acc[k] += h.cover[k];
+  }
+  int rc = allreduce_u64(x, acc.data(), 2 * COVER_CODES, 0);
+  if (rc) return rc;
   for (int k = 0; k < n && k < COVER_CODES; k++) {
-    if (gen) gen[k] = h.cover[k];
-    if (distinct) distinct[k] = h.cover[COVER_CODES + k];
+    if (gen) gen[k] = acc[k];
+    if (distinct) distinct[k] = acc[COVER_CODES + k];
   }
   return COVER_CODES;
 }
 
-// Counterexample: walk parent pointers back to Init, then replay the action
-// instances forward from the Init row with the same kernel that built them.
+// Counterexample (on the shard that found the violation): walk its parent
+// pointers back to Init, then replay the action instances forward from the
+// Init row with the kernel that built them.
 extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t cap, size_t* n_rows) {
   if (!x || !n_rows) return RTLA_E_ARG;
-  if (!x->viol_mask) return RTLA_E_STATE;
+  Shard* s = viol_shard(x);
+  if (!s) return RTLA_E_STATE;
   HIPCHK(hipSetDevice(x->device));
   const Layout& L = x->L;
-  std::vector<int32_t> insts;  // forward order after reversal
+  std::vector<int32_t> insts;
   uint64_t g;
-  if (x->viol_inst < 0) {
-    g = 0;  // Init itself
-  } else if (x->viol_in_model && x->viol_child != ~0ull) {
-    g = x->viol_child;
+  if (s->viol_inst < 0) {
+    g = 0;
+  } else if (s->viol_in_model && s->viol_child != ~0ull) {
+    g = s->viol_child;
   } else {
-    insts.push_back(x->viol_inst);
-    g = x->viol_parent;
+    insts.push_back(s->viol_inst);
+    g = s->viol_parent;
   }
-  while (g != 0) {
+  while (true) {
     uint64_t p;
-    HIPCHK(hipMemcpy(&p, x->parents + g, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&p, s->parents + g, 8, hipMemcpyDeviceToHost));
+    if (p == ~0ull) break;  // Init
     insts.push_back((int32_t)(p & 0xffff));
     g = p >> 16;
   }
   std::reverse(insts.begin(), insts.end());
   size_t n = insts.size() + 1;
   *n_rows = n;
+  if (!rows && !labels) return RTLA_OK;
   if (n > cap) return RTLA_E_ARG;
   std::vector<uint32_t> row = x->init_row;
   uint32_t* d_row = nullptr;
   HIPCHK(hipMalloc(&d_row, L.W * 4));
   if (rows) memcpy(rows, row.data(), L.W * 4);
   if (labels) labels[0] = -1;
-  for (size_t k = 0; k < insts.size(); k++) {
-    HIPCHK(hipMemcpy(d_row, row.data(), L.W * 4, hipMemcpyHostToDevice));
+  int rc = RTLA_OK;
+  for (size_t k = 0; k < insts.size() && rc == RTLA_OK; k++) {
+    if (hipMemcpy(d_row, row.data(), L.W * 4, hipMemcpyHostToDevice) != hipSuccess) { rc = RTLA_E_HIP; break; }
     std::vector<uint32_t> out;
     std::vector<uint64_t> info;
     int r = expand_batch_dev(L, d_row, 1, out, info, x->stream);
-    if (r < 0) { hipFree(d_row); return r; }
+    if (r < 0) { rc = r; break; }
     size_t hit = info.size();
     for (size_t q = 0; q < info.size(); q++)
       if ((int32_t)(info[q] & 0xffff) == insts[k]) hit = q;
-    if (hit == info.size()) { hipFree(d_row); return RTLA_E_STATE; }
+    if (hit == info.size()) { rc = RTLA_E_STATE; break; }
     memcpy(row.data(), &out[hit * L.W], L.W * 4);
     if (rows) memcpy(rows + (k + 1) * L.W, row.data(), L.W * 4);
-    if (labels) labels[k + 1] = (int32_t)(info[hit] & 0xffffffffu & ~(1u << 31));
+    if (labels) labels[k + 1] = (int32_t)(info[hit] & 0x7fffffffu);
   }
-  hipFree(d_row);
-  return RTLA_OK;
+  (void)hipFree(d_row);
+  return rc;
 }
 
 extern "C" int rtla_probe_bench(int log2, uint64_t n, double* seconds, uint64_t* inserted) {
@@ -481,23 +772,25 @@ extern "C" int rtla_probe_bench(int log2, uint64_t n, double* seconds, uint64_t*
   HIPCHK(hipMemset(table, 0, 8ull << log2));
   HIPCHK(hipMemset(ctr, 0, sizeof(DevCounters)));
   hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
   HIPCHK(launch_probe_bench(table, log2, n / 8, 12345, ctr, nullptr));  // warm
   HIPCHK(hipMemset(table, 0, 8ull << log2));
   HIPCHK(hipMemset(ctr, 0, sizeof(DevCounters)));
   HIPCHK(hipDeviceSynchronize());
-  hipEventRecord(a, nullptr);
+  HIPCHK(hipEventRecord(a, nullptr));
   HIPCHK(launch_probe_bench(table, log2, n, 777, ctr, nullptr));
-  hipEventRecord(b, nullptr);
+  HIPCHK(hipEventRecord(b, nullptr));
   HIPCHK(hipEventSynchronize(b));
   float ms = 0;
-  hipEventElapsedTime(&ms, a, b);
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
   DevCounters h;
   HIPCHK(hipMemcpy(&h, ctr, sizeof h, hipMemcpyDeviceToHost));
   if (seconds) *seconds = ms / 1e3;
   if (inserted) *inserted = h.next_count;
-  hipEventDestroy(a); hipEventDestroy(b);
-  hipFree(table); hipFree(ctr);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(table);
+  (void)hipFree(ctr);
   return RTLA_OK;
 }

@@ -16,6 +16,8 @@
 //   * invariants are checked on every new and every out-of-model successor.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rtla_device.h"
 #include "rtla_model.h"
 
@@ -77,10 +79,11 @@ __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
 
 // LDS per wave: parent row (W) + new allLogs words (32) + staging (64 rows x W).
 extern "C" __global__ void __launch_bounds__(256)
-k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long n_cur,
+k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
          unsigned long long cur_base, uint32_t* __restrict__ next,
          unsigned long long* __restrict__ parents, unsigned long long next_base,
-         unsigned long long next_cap, unsigned long long* table, int tlog2, DevCounters* ctr) {
+         unsigned long long next_cap, unsigned long long* table, int tlog2, DevCounters* ctr,
+         ShardBox box) {
   extern __shared__ uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -94,7 +97,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long n_cur,
 
   unsigned long long my_gen = 0, my_probe = 0;
   const int fixed = L.fam[F_RECEIVE];
-  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wave; s < n_cur;
+  for (unsigned long long s = s_begin + (unsigned long long)blockIdx.x * wpb + wave; s < s_end;
        s += (unsigned long long)gridDim.x * wpb) {
     const uint32_t* src = cur + s * (unsigned long long)W;
     for (int w = lane; w < W; w += 64) prow[w] = src[w];
@@ -126,10 +129,25 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long n_cur,
       FP cfp{0, 0};
       if (en && d.in_model) {
         cfp = fp_add(pfp, delta_fp(L, prow, d));
-        my_probe++;
-        int r = fpset_insert(table, tlog2, cfp);
-        if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
-        isnew = r == 1;
+        const int owner = fp_owner(cfp, box.nshard);
+        if (owner == box.me) {
+          my_probe++;
+          int r = fpset_insert(table, tlog2, cfp);
+          if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
+          isnew = r == 1;
+        } else {
+          // Another shard owns this fingerprint: queue (fp, parent, instance);
+          // the owner answers new/seen and this shard materialises the winner.
+          unsigned long long slot = atomicAdd(&box.out_count[owner], 1ull);
+          if (slot < box.cap) {
+            unsigned long long k = (unsigned long long)owner * box.cap + slot;
+            box.send_fp[2 * k] = cfp.a;
+            box.send_fp[2 * k + 1] = cfp.b;
+            box.send_ref[k] = s << 16 | (unsigned long long)inst;
+          } else {
+            set_flag(ctr, FLAG_OUTBOX_FULL);
+          }
+        }
       }
       if (en) {
         int code = cover_code(L, inst, d.sub);
@@ -178,13 +196,77 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long n_cur,
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
+// Owner side of the exchange: insert the fingerprints other shards sent,
+// answer 1 (new) / 0 (seen) per record.  Region p holds count[p] records.
+extern "C" __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
+                                           const unsigned long long* __restrict__ counts, int nshard,
+                                           unsigned long long cap, unsigned long long* table, int tlog2,
+                                           uint8_t* __restrict__ res, DevCounters* ctr) {
+  unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+  unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  unsigned long long probes = 0;
+  for (; i < (unsigned long long)nshard * cap; i += stride) {
+    unsigned long long p = i / cap, k = i - p * cap;
+    if (k >= counts[p]) continue;
+    FP f{recv_fp[2 * i], recv_fp[2 * i + 1]};
+    int r = fpset_insert(table, tlog2, f);
+    if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
+    res[i] = r == 1 ? 1 : 0;
+    probes++;
+  }
+  for (int off = 32; off > 0; off >>= 1) probes += __shfl_down(probes, off);
+  if ((threadIdx.x & 63) == 0 && probes) atomicAdd(&ctr->probes, probes);
+}
+
+// Sender side, after the owners answered: materialise every queued successor
+// whose fingerprint was new at its owner.  The state lives on this shard, next
+// to its parent, so parent pointers (and traces) stay shard-local.
+extern "C" __global__ void k_materialize(Layout L, const uint32_t* __restrict__ cur,
+                                         unsigned long long cur_base,
+                                         const unsigned long long* __restrict__ send_ref,
+                                         const uint8_t* __restrict__ res,
+                                         const unsigned long long* __restrict__ counts, int nshard,
+                                         unsigned long long cap, uint32_t* __restrict__ next,
+                                         unsigned long long* __restrict__ parents,
+                                         unsigned long long next_base, unsigned long long next_cap,
+                                         DevCounters* ctr) {
+  unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+  unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  uint32_t all_new[32];
+  for (; i < (unsigned long long)nshard * cap; i += stride) {
+    unsigned long long p = i / cap, k = i - p * cap;
+    if (k >= counts[p] || !res[i]) continue;
+    unsigned long long ref = send_ref[i];
+    unsigned long long s = ref >> 16;
+    int inst = (int)(ref & 0xffff);
+    const uint32_t* prow = cur + s * (unsigned long long)L.W;
+    Delta d;
+    compute_delta(L, prow, inst, d);
+    FP afp = alllogs_delta(L, prow, all_new);
+    FP cfp = fp_add(fp_add(row_fp(prow), afp), delta_fp(L, prow, d));
+    unsigned long long o = atomicAdd(&ctr->next_count, 1ull);
+    if (o >= next_cap) { set_flag(ctr, FLAG_FRONTIER_FULL); continue; }
+    materialize(L, prow, d, all_new, cfp, next + o * (unsigned long long)L.W);
+    parents[next_base + o] = (cur_base + s) << 16 | (unsigned long long)inst;
+    int code = cover_code(L, inst, d.sub);
+    atomicAdd(&ctr->cover[COVER_CODES + code], 1ull);
+    int bad = check_invariants(L, prow, &d);
+    if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+      ctr->viol_parent = cur_base + s;
+      ctr->viol_inst = inst;
+      ctr->viol_in_model = 1;
+      ctr->viol_child = next_base + o;
+    }
+  }
+}
+
 // Insert the fingerprints of `n` rows (Init).  new_flags[i] = 1 if new.
 extern "C" __global__ void k_insert_rows(Layout L, const uint32_t* rows, unsigned long long n,
                                          unsigned long long* table, int tlog2, int* new_flags,
                                          DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  FP f = row_fp(rows + i * (unsigned long long)L.W);
+  FP f = row_fp(rows + (unsigned long long)i * L.W);
   int r = fpset_insert(table, tlog2, f);
   if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
   new_flags[i] = r == 1;
@@ -281,14 +363,39 @@ int expand_blocks_per_cu(const Layout& L) {
   return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
 
-hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t n_cur, uint64_t cur_base,
-                         uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
-                         uint64_t* table, int tlog2, DevCounters* ctr, int grid, hipStream_t st) {
-  if (n_cur == 0) return hipSuccess;
+hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end,
+                         uint64_t cur_base, uint32_t* next, uint64_t* parents, uint64_t next_base,
+                         uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
+                         int grid, hipStream_t st) {
+  if (s_end <= s_begin) return hipSuccess;
   hipLaunchKernelGGL(k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
-                     (unsigned long long)n_cur, (unsigned long long)cur_base, next,
+                     (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base,
+                     next, (unsigned long long*)parents, (unsigned long long)next_base,
+                     (unsigned long long)next_cap, (unsigned long long*)table, tlog2, ctr, box);
+  return hipGetLastError();
+}
+
+hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
+                                uint64_t* table, int tlog2, uint8_t* res, DevCounters* ctr, hipStream_t st) {
+  uint64_t n = (uint64_t)nshard * cap;
+  uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_insert_remote, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (const unsigned long long*)recv_fp, (const unsigned long long*)counts, nshard,
+                     (unsigned long long)cap, (unsigned long long*)table, tlog2, res, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_materialize(const Layout& L, const uint32_t* cur, uint64_t cur_base, const uint64_t* send_ref,
+                              const uint8_t* res, const uint64_t* counts, int nshard, uint64_t cap,
+                              uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                              DevCounters* ctr, hipStream_t st) {
+  uint64_t n = (uint64_t)nshard * cap;
+  uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_materialize, dim3((unsigned)blocks), dim3(256), 0, st, L, cur,
+                     (unsigned long long)cur_base, (const unsigned long long*)send_ref, res,
+                     (const unsigned long long*)counts, nshard, (unsigned long long)cap, next,
                      (unsigned long long*)parents, (unsigned long long)next_base,
-                     (unsigned long long)next_cap, (unsigned long long*)table, tlog2, ctr);
+                     (unsigned long long)next_cap, ctr);
   return hipGetLastError();
 }
 

@@ -12,9 +12,16 @@ size_t expand_lds_bytes(const Layout& L, int wpb);
 // Blocks of 4 waves that fit on one CU given the LDS footprint.
 int expand_blocks_per_cu(const Layout& L);
 
-hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t n_cur, uint64_t cur_base,
-                         uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
-                         uint64_t* table, int tlog2, DevCounters* ctr, int grid, hipStream_t st);
+hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end,
+                         uint64_t cur_base, uint32_t* next, uint64_t* parents, uint64_t next_base,
+                         uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
+                         int grid, hipStream_t st);
+hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
+                                uint64_t* table, int tlog2, uint8_t* res, DevCounters* ctr, hipStream_t st);
+hipError_t launch_materialize(const Layout& L, const uint32_t* cur, uint64_t cur_base, const uint64_t* send_ref,
+                              const uint8_t* res, const uint64_t* counts, int nshard, uint64_t cap,
+                              uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                              DevCounters* ctr, hipStream_t st);
 hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
                               int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st);
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,

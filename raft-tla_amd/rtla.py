@@ -42,8 +42,8 @@ class _Cfg(C.Structure):
     _fields_ = [("n_server", C.c_int32), ("n_value", C.c_int32), ("max_term", C.c_int32),
                 ("max_log", C.c_int32), ("max_copies", C.c_int32), ("max_msgs", C.c_int32),
                 ("bag_cap", C.c_int32), ("elec_cap", C.c_int32), ("inv_mask", C.c_int32),
-                ("symmetry", C.c_int32), ("fpset_log2", C.c_int32), ("reserved", C.c_int32),
-                ("frontier_cap", C.c_uint64), ("mem_budget", C.c_uint64)]
+                ("symmetry", C.c_int32), ("fpset_log2", C.c_int32), ("shards", C.c_int32),
+                ("frontier_cap", C.c_uint64), ("mem_budget", C.c_uint64), ("chunk", C.c_uint64)]
 
 
 class _Stats(C.Structure):
@@ -113,6 +113,8 @@ class Config:
     fpset_log2: int = 0
     frontier_cap: int = 0
     mem_budget: int = 0
+    shards: int = 0
+    chunk: int = 0
 
     @property
     def inv_mask(self) -> int:
@@ -124,7 +126,7 @@ class Config:
     def c(self) -> _Cfg:
         return _Cfg(self.n_server, self.n_value, self.max_term, self.max_log, self.max_copies,
                     self.max_msgs, self.bag_cap, self.elec_cap, self.inv_mask, 0,
-                    self.fpset_log2, 0, self.frontier_cap, self.mem_budget)
+                    self.fpset_log2, self.shards, self.frontier_cap, self.mem_budget, self.chunk)
 
 
 @dataclass
@@ -339,6 +341,13 @@ def check(cfg: Config, trace: bool = True) -> Result:
             if trace:
                 res.trace = ck.trace()
         return res
+
+
+def comm_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 makes it, every rank passes it to Checker)."""
+    buf = C.create_string_buffer(128)
+    _check(_lib.rtla_comm_id(buf), "rtla_comm_id")
+    return buf.raw
 
 
 def probe_bench(log2: int, n: int):

@@ -172,3 +172,50 @@ def test_full_size_counts_match_golden(name):
 def test_fpset_probe_bench_inserts_all():
     sec, ins = rtla.probe_bench(26, 1 << 24)
     assert ins == 1 << 24 and sec > 0
+
+
+# ---- fingerprint-sharded search (the multi-GPU protocol on one device) ----
+SHARDED = ["n2_v2_t3_l2_m1", "n3_v1_t2_l1_m1", "n2_v1_t2_l1_c2_m2", "n1_v2_t3_l2"]
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+@pytest.mark.parametrize("name", SHARDED)
+def test_virtual_shards_match_golden(name, shards):
+    """S fingerprint-owned shards exchanging (fp -> owner, answer -> sender,
+    sender materialises) must give the single-shard counts at every level,
+    also when each level is cut into many exchange rounds (small chunk)."""
+    g = GOLD[name]
+    kw = small_kw(g)
+    kw["mem_budget"] *= shards
+    res = rtla.check(cfg_of(g, shards=shards, chunk=512, **kw), trace=False)
+    assert [[lv.new, lv.generated] for lv in res.levels] == g["levels"]
+    assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+
+
+def test_virtual_shards_level_contents():
+    g = GOLD["n2_v2_t3_l2_m1"]
+    kw = small_kw(g)
+    kw["mem_budget"] *= 4
+    cfg = cfg_of(g, shards=4, chunk=1000, **kw)
+    got = []
+    with rtla.Checker(cfg) as ck:
+        st = ck.init()
+        while True:
+            rows = ck.frontier()
+            got.append("%016x" % (sum(rv.fnv1a64(rtla.state_text(cfg, r)) for r in rows) & (2**64 - 1)))
+            if st != rtla.OK:
+                break
+            st = ck.step()
+    assert got[:len(g["level_text_hash"])] == g["level_text_hash"]
+
+
+def test_virtual_shards_trace():
+    g = GOLD["n3_v1_t3_l1_m1_ntl"]
+    kw = small_kw(g)
+    kw["mem_budget"] *= 4
+    res = rtla.check(cfg_of(g, shards=4, **kw))
+    assert res.violation == "NoTwoLeaders" and len(res.trace) == g["depth"]
+    walk = raft_cpu.Walk(raft_cpu.cfg_of(3, 1, 3, 1, 1, 1, ("NoTwoLeaders",)))
+    for label, text in res.trace[1:]:
+        walk.goto(text)
+    assert walk.invariants() & 1
