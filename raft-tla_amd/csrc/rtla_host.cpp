@@ -5,7 +5,7 @@
 // owns (fp_owner, rtla_device.h), the states it materialised (frontier double
 // buffer) and their parent pointers.  Device memory per shard:
 //   fingerprint set   2^fpset_log2 x 8 B   (open addressing, CAS insert)
-//   parents           one u64 per state: parent shard-local index << 16 | instance
+//   parents           one u64 per state: parent shard << 56 | parent index << 16 | instance
 //   frontier A / B    frontier_cap rows each (double buffer, swapped per level)
 //   outbox / inbox    (multi-shard only) per destination: fingerprints, refs, answers
 //
@@ -23,10 +23,15 @@
 //   2. all-gather of the per-destination counts, then all-to-all-v of the
 //      16-byte fingerprints (ncclSend/ncclRecv pairs in one group: all 7 xGMI
 //      links of an MI355X node carry traffic at once);
-//   3. k_insert_remote at the owner answers new/seen (1 byte per record);
-//   4. all-to-all-v of the answers back;
-//   5. k_materialize at the sender builds the winners next to their parents,
-//      so traces never cross shards.
+//   3. k_insert_remote at the owner answers each record with 0 (seen) or
+//      1 + a dense rank among the new fingerprints from that sender;
+//   4. all-to-all-v of the answers back, all-gather of the winner counts;
+//   5. k_pack_rows at the sender materialises the winners (it holds the
+//      parent row) into the owner's row region at their rank, one all-to-all-v
+//      ships the rows, k_unpack_rows appends them to the owner's next
+//      frontier.  New states therefore live on their owner shard, which
+//      spreads the next level's expansion evenly; parent records name the
+//      parent's shard, so traces walk across shards.
 // Then one all-reduce of {new, generated, probes, violation, flags} decides
 // termination (TLC's "0 states left on queue").
 #include <hip/hip_runtime.h>
@@ -65,10 +70,15 @@ struct Shard {
   uint64_t* all_count = nullptr;   // [G][G] device (RCCL all-gather target)
   uint64_t* send_fp = nullptr;     // [G][cap][2]
   uint64_t* send_ref = nullptr;    // [G][cap]
-  uint8_t* send_res = nullptr;     // [G][cap]
+  uint32_t* send_ans = nullptr;    // [G][cap]  owners' answers to our records
   uint64_t* recv_fp = nullptr;     // [G][cap][2]
-  uint8_t* recv_res = nullptr;     // [G][cap]
-  std::vector<uint64_t> h_out, h_in;
+  uint32_t* recv_ans = nullptr;    // [G][cap]  our answers to the senders
+  uint64_t* new_count = nullptr;   // [G] device: new fingerprints we own, per source
+  uint64_t* all_new = nullptr;     // [G][G] device (RCCL all-gather target)
+  uint64_t* rows_in = nullptr;     // [G] device: rows received per source (this sub-round)
+  uint32_t* send_rows = nullptr;   // [G][rows_cap][W + 2]
+  uint32_t* recv_rows = nullptr;   // [G][rows_cap][W + 2]
+  std::vector<uint64_t> h_out, h_in, h_new_out, h_new_in;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // violation found on this shard
   int viol_mask = 0, viol_in_model = 0, viol_inst = -1;
@@ -87,7 +97,7 @@ struct rtla_ctx {
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   int tlog2 = 0;
-  uint64_t front_cap = 0, box_cap = 0, chunk = 0;
+  uint64_t front_cap = 0, box_cap = 0, chunk = 0, rows_cap = 0;
   uint64_t* red = nullptr;  // device scratch for all-reduces
   int level = 0;
   bool inited = false, finished = false;
@@ -274,8 +284,9 @@ extern "C" int rtla_comm_id(void* out128) {
 }
 
 static void free_shard(Shard& s) {
-  void* ptrs[] = {s.table, s.parents, s.front[0], s.front[1], s.ctr, s.dflags, s.out_count, s.in_count,
-                  s.all_count, s.send_fp, s.send_ref, s.send_res, s.recv_fp, s.recv_res};
+  void* ptrs[] = {s.table,    s.parents,  s.front[0], s.front[1], s.ctr,       s.dflags,    s.out_count,
+                  s.in_count, s.all_count, s.send_fp, s.send_ref, s.send_ans,  s.recv_fp,   s.recv_ans,
+                  s.new_count, s.all_new, s.rows_in,  s.send_rows, s.recv_rows};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -300,7 +311,9 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   s.parents_cap = (1ull << x->tlog2) - (1ull << x->tlog2) / 4;  // load factor <= 0.75
   uint64_t pbytes = s.parents_cap * 8;
   uint64_t rowb = (uint64_t)L.W * 4;
-  uint64_t boxb = G > 1 ? (uint64_t)G * x->box_cap * (16 + 8 + 1 + 16 + 1) : 0;
+  uint64_t boxb = G > 1 ? (uint64_t)G * x->box_cap * (16 + 8 + 4 + 16 + 4) +
+                              2ull * G * x->rows_cap * (L.W + 2) * 4
+                        : 0;
   if (!x->front_cap) {
     uint64_t used = tbytes + pbytes + boxb;
     uint64_t rest = budget > used ? budget - used : 0;
@@ -318,11 +331,18 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
     HIPCHK(hipMalloc(&s.all_count, 8 * G * G));
     HIPCHK(hipMalloc(&s.send_fp, 16 * G * x->box_cap));
     HIPCHK(hipMalloc(&s.send_ref, 8 * G * x->box_cap));
-    HIPCHK(hipMalloc(&s.send_res, G * x->box_cap));
+    HIPCHK(hipMalloc(&s.send_ans, 4 * G * x->box_cap));
     HIPCHK(hipMalloc(&s.recv_fp, 16 * G * x->box_cap));
-    HIPCHK(hipMalloc(&s.recv_res, G * x->box_cap));
+    HIPCHK(hipMalloc(&s.recv_ans, 4 * G * x->box_cap));
+    HIPCHK(hipMalloc(&s.new_count, 8 * G));
+    HIPCHK(hipMalloc(&s.all_new, 8 * G * G));
+    HIPCHK(hipMalloc(&s.rows_in, 8 * G));
+    HIPCHK(hipMalloc(&s.send_rows, 4ull * G * x->rows_cap * (L.W + 2)));
+    HIPCHK(hipMalloc(&s.recv_rows, 4ull * G * x->rows_cap * (L.W + 2)));
     s.h_out.assign(G, 0);
     s.h_in.assign(G, 0);
+    s.h_new_out.assign(G, 0);
+    s.h_new_in.assign(G, 0);
   }
   HIPCHK(hipMemsetAsync(s.table, 0, tbytes, x->stream));
   HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
@@ -367,10 +387,13 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
     uint64_t nmax = (uint64_t)(L.fam[F_RECEIVE] + 3 * L.K);
     x->chunk = cfg->chunk;
     if (!x->chunk) {
-      x->chunk = (per / 8) / ((uint64_t)G * nmax * 42);
+      x->chunk = (per / 8) / ((uint64_t)G * nmax * 48);
       x->chunk = std::min<uint64_t>(std::max<uint64_t>(x->chunk, 1024), 1u << 20);
     }
     x->box_cap = x->chunk * nmax;
+    // row regions: ~1/10 of the budget; winners beyond it ship in sub-rounds
+    x->rows_cap = (per / 10) / (2ull * G * (L.W + 2) * 4);
+    x->rows_cap = std::min<uint64_t>(std::max<uint64_t>(x->rows_cap, 256), x->box_cap);
   }
   int tl = cfg->fpset_log2;
   if (!tl) {
@@ -515,28 +538,78 @@ static int exchange_fps(rtla_ctx* x) {
   return RTLA_OK;
 }
 
-// Owners answered in recv_res; route the answers back into send_res.
+// Owners answered in recv_ans (0 = seen, 1 + rank = new); route the answers
+// back into send_ans and tell every sender how many winners each owner has
+// from it (h_new_out) and every owner how many rows to expect (h_new_in).
 static int exchange_answers(rtla_ctx* x) {
   const int G = x->nshard;
   const uint64_t cap = x->box_cap;
   if (x->world == 1) {
+    for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.new_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
     for (auto& src : x->sh)
       for (auto& dst : x->sh) {
         uint64_t n = src.h_out[dst.id];
         if (n)
-          HIPCHK(hipMemcpyAsync(src.send_res + (uint64_t)dst.id * cap, dst.recv_res + (uint64_t)src.id * cap, n,
+          HIPCHK(hipMemcpyAsync(src.send_ans + (uint64_t)dst.id * cap, dst.recv_ans + (uint64_t)src.id * cap, 4 * n,
                                 hipMemcpyDeviceToDevice, x->stream));
       }
+    HIPCHK(hipStreamSynchronize(x->stream));
+    for (auto& src : x->sh)
+      for (auto& dst : x->sh) src.h_new_out[dst.id] = dst.h_new_in[src.id];
     return RTLA_OK;
   }
   Shard& s = x->sh[0];
   NCCLCHK(ncclGroupStart());
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
-    NCCLCHK(ncclSend(s.recv_res + (uint64_t)p * cap, s.h_in[p], ncclUint8, p, x->comm, x->stream));
-    NCCLCHK(ncclRecv(s.send_res + (uint64_t)p * cap, s.h_out[p], ncclUint8, p, x->comm, x->stream));
+    NCCLCHK(ncclSend(s.recv_ans + (uint64_t)p * cap, s.h_in[p], ncclUint32, p, x->comm, x->stream));
+    NCCLCHK(ncclRecv(s.send_ans + (uint64_t)p * cap, s.h_out[p], ncclUint32, p, x->comm, x->stream));
   }
   NCCLCHK(ncclGroupEnd());
+  NCCLCHK(ncclAllGather(s.new_count, s.all_new, G, ncclUint64, x->comm, x->stream));
+  std::vector<uint64_t> all((size_t)G * G);
+  HIPCHK(hipMemcpyAsync(all.data(), s.all_new, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  for (int p = 0; p < G; p++) {
+    s.h_new_in[p] = all[(size_t)s.id * G + p];   // owner s.id: new from source p
+    s.h_new_out[p] = all[(size_t)p * G + s.id];  // owner p: new from us
+  }
+  return RTLA_OK;
+}
+
+// Ship the winners of ranks [lo, lo + rows_cap) to their owners.
+static int exchange_rows(rtla_ctx* x, uint64_t lo) {
+  const int G = x->nshard;
+  const uint64_t rc = x->rows_cap, RW = (uint64_t)x->L.W + 2;
+  auto part = [&](uint64_t n) { return n > lo ? std::min<uint64_t>(n - lo, rc) : 0; };
+  if (x->world == 1) {
+    for (auto& dst : x->sh) {
+      std::vector<uint64_t> in(G, 0);
+      for (auto& src : x->sh) {
+        uint64_t n = part(src.h_new_out[dst.id]);
+        in[src.id] = n;
+        if (n)
+          HIPCHK(hipMemcpyAsync(dst.recv_rows + (uint64_t)src.id * rc * RW, src.send_rows + (uint64_t)dst.id * rc * RW,
+                                4 * n * RW, hipMemcpyDeviceToDevice, x->stream));
+      }
+      HIPCHK(hipMemcpyAsync(dst.rows_in, in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
+      HIPCHK(hipStreamSynchronize(x->stream));  // `in` is a host temporary
+    }
+    return RTLA_OK;
+  }
+  Shard& s = x->sh[0];
+  std::vector<uint64_t> in(G, 0);
+  for (int p = 0; p < G; p++) in[p] = part(s.h_new_in[p]);
+  HIPCHK(hipMemcpyAsync(s.rows_in, in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
+  NCCLCHK(ncclGroupStart());
+  for (int p = 0; p < G; p++) {
+    if (p == s.id) continue;
+    NCCLCHK(ncclSend(s.send_rows + (uint64_t)p * rc * RW, part(s.h_new_out[p]) * RW, ncclUint32, p, x->comm,
+                     x->stream));
+    NCCLCHK(ncclRecv(s.recv_rows + (uint64_t)p * rc * RW, in[p] * RW, ncclUint32, p, x->comm, x->stream));
+  }
+  NCCLCHK(ncclGroupEnd());
+  HIPCHK(hipStreamSynchronize(x->stream));
   return RTLA_OK;
 }
 
@@ -593,15 +666,31 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
           }
       rc = exchange_fps(x);
       if (rc) return rc;
-      for (auto& s : x->sh)
-        HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_res, s.ctr,
-                                    x->stream));
+      for (auto& s : x->sh) {
+        HIPCHK(hipMemsetAsync(s.new_count, 0, 8 * G, x->stream));
+        HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_ans, s.new_count,
+                                    s.ctr, x->stream));
+      }
       rc = exchange_answers(x);
       if (rc) return rc;
-      for (size_t k = 0; k < x->sh.size(); k++) {
-        Shard& s = x->sh[k];
-        HIPCHK(launch_materialize(L, s.front[s.cur], s.cur_base, s.send_ref, s.send_res, s.out_count, G, x->box_cap,
-                                  s.front[s.cur ^ 1], s.parents, next_base[k], next_cap[k], s.ctr, x->stream));
+      uint64_t most = 0;
+      for (auto& s : x->sh)
+        for (int p = 0; p < G; p++) most = std::max(most, std::max(s.h_new_out[p], s.h_new_in[p]));
+      rc = allreduce_u64(x, &most, 1, 1);
+      if (rc) return rc;
+      for (uint64_t lo = 0; lo < most; lo += x->rows_cap) {
+        for (size_t k = 0; k < x->sh.size(); k++) {
+          Shard& s = x->sh[k];
+          HIPCHK(launch_pack_rows(L, s.front[s.cur], s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
+                                  x->box_cap, lo, lo + x->rows_cap, s.send_rows, x->rows_cap, s.ctr, x->stream));
+        }
+        rc = exchange_rows(x, lo);
+        if (rc) return rc;
+        for (size_t k = 0; k < x->sh.size(); k++) {
+          Shard& s = x->sh[k];
+          HIPCHK(launch_unpack_rows(L.W, s.recv_rows, s.rows_in, G, x->rows_cap, s.front[s.cur ^ 1], s.parents,
+                                    next_base[k], next_cap[k], s.ctr, x->stream));
+        }
       }
     }
   }
@@ -659,7 +748,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   return status;
 }
 
-static Shard* viol_shard(rtla_ctx* x) {
+static Shard* viol_shard(rtla_ctx* x) {  // violation found on a local shard
   for (auto& s : x->sh)
     if (s.viol_mask) return &s;
   return nullptr;
@@ -709,31 +798,60 @@ extern "C" int rtla_coverage(rtla_ctx* x, uint64_t* gen, uint64_t* distinct, int
   return COVER_CODES;
 }
 
-// Counterexample (on the shard that found the violation): walk its parent
-// pointers back to Init, then replay the action instances forward from the
-// Init row with the kernel that built them.
+// Counterexample: find the violating state (or its parent + action when the
+// violation was seen before the state had a home), walk the parent records
+// back to Init -- across shards: a record is shard << 56 | index << 16 |
+// instance -- then replay the action instances forward from the Init row with
+// the kernel that built them.  Collective when world > 1 (every rank calls it;
+// each step's record is broadcast by the rank that holds it).
 extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t cap, size_t* n_rows) {
   if (!x || !n_rows) return RTLA_E_ARG;
-  Shard* s = viol_shard(x);
-  if (!s) return RTLA_E_STATE;
   HIPCHK(hipSetDevice(x->device));
   const Layout& L = x->L;
-  std::vector<int32_t> insts;
-  uint64_t g;
-  if (s->viol_inst < 0) {
-    g = 0;
-  } else if (s->viol_in_model && s->viol_child != ~0ull) {
-    g = s->viol_child;
-  } else {
-    insts.push_back(s->viol_inst);
-    g = s->viol_parent;
+  // start: (holder shard, shard-local index, pending instance or -1)
+  uint64_t start[4] = {0, 0, 0, 0};  // has, shard, g, inst + 1
+  Shard* vs = nullptr;
+  for (auto& s : x->sh)
+    if (s.viol_mask) { vs = &s; break; }
+  if (vs) {
+    start[0] = 1;
+    start[1] = (uint64_t)vs->id;
+    if (vs->viol_inst < 0) { start[2] = 0; start[3] = 0; }
+    else if (vs->viol_in_model && vs->viol_child != ~0ull) { start[2] = vs->viol_child; start[3] = 0; }
+    else { start[2] = vs->viol_parent; start[3] = (uint64_t)vs->viol_inst + 1; }
   }
-  while (true) {
-    uint64_t p;
-    HIPCHK(hipMemcpy(&p, s->parents + g, 8, hipMemcpyDeviceToHost));
+  if (x->world > 1) {
+    // the lowest shard holding a violation publishes its start record
+    uint64_t holder = start[0] ? start[1] : (uint64_t)x->nshard;
+    uint64_t mn = (uint64_t)x->nshard - holder;  // max of (G - holder) == min holder
+    int rc = allreduce_u64(x, &mn, 1, 1);
+    if (rc) return rc;
+    if (mn == 0) return RTLA_E_STATE;
+    int root = (int)((uint64_t)x->nshard - mn);
+    HIPCHK(hipMemcpyAsync(x->red, start, 32, hipMemcpyHostToDevice, x->stream));
+    NCCLCHK(ncclBroadcast(x->red, x->red, 4, ncclUint64, root, x->comm, x->stream));
+    HIPCHK(hipMemcpyAsync(start, x->red, 32, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+  } else if (!start[0]) {
+    return RTLA_E_STATE;
+  }
+  std::vector<int32_t> insts;
+  if (start[3]) insts.push_back((int32_t)(start[3] - 1));
+  uint64_t shard = start[1], g = start[2];
+  for (int guard = 0; guard < (1 << 20); guard++) {
+    uint64_t p = 0;
+    if (x->world == 1) {
+      HIPCHK(hipMemcpy(&p, x->sh[shard].parents + g, 8, hipMemcpyDeviceToHost));
+    } else {
+      if ((int)shard == x->rank) HIPCHK(hipMemcpyAsync(x->red, x->sh[0].parents + g, 8, hipMemcpyDeviceToDevice, x->stream));
+      NCCLCHK(ncclBroadcast(x->red, x->red, 1, ncclUint64, (int)shard, x->comm, x->stream));
+      HIPCHK(hipMemcpyAsync(&p, x->red, 8, hipMemcpyDeviceToHost, x->stream));
+      HIPCHK(hipStreamSynchronize(x->stream));
+    }
     if (p == ~0ull) break;  // Init
     insts.push_back((int32_t)(p & 0xffff));
-    g = p >> 16;
+    shard = p >> 56;
+    g = (p >> 16) & ((1ull << 40) - 1);
   }
   std::reverse(insts.begin(), insts.end());
   size_t n = insts.size() + 1;

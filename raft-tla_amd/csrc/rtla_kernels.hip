@@ -167,7 +167,9 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
         if (obase + cnt <= next_cap) {
           uint32_t* dst = next + obase * (unsigned long long)W;
           for (int w = lane; w < cnt * W; w += 64) dst[w] = stage[w];
-          if (isnew) parents[next_base + obase + rank] = (cur_base + s) << 16 | (unsigned long long)inst;
+          if (isnew)
+            parents[next_base + obase + rank] =
+                (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
         } else if (lane == 0) {
           set_flag(ctr, FLAG_FRONTIER_FULL);
         }
@@ -196,12 +198,15 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
-// Owner side of the exchange: insert the fingerprints other shards sent,
-// answer 1 (new) / 0 (seen) per record.  Region p holds count[p] records.
+// Owner side of the exchange: insert the fingerprints other shards sent and
+// answer each record with 0 (seen) or 1 + its dense rank among the new
+// fingerprints from that source (the sender uses the rank as the row slot it
+// ships the materialised state into).  Region p holds counts[p] records.
 extern "C" __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
                                            const unsigned long long* __restrict__ counts, int nshard,
                                            unsigned long long cap, unsigned long long* table, int tlog2,
-                                           uint8_t* __restrict__ res, DevCounters* ctr) {
+                                           uint32_t* __restrict__ ans, unsigned long long* __restrict__ new_count,
+                                           DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   unsigned long long probes = 0;
@@ -211,31 +216,32 @@ extern "C" __global__ void k_insert_remote(const unsigned long long* __restrict_
     FP f{recv_fp[2 * i], recv_fp[2 * i + 1]};
     int r = fpset_insert(table, tlog2, f);
     if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
-    res[i] = r == 1 ? 1 : 0;
+    ans[i] = r == 1 ? (uint32_t)atomicAdd(&new_count[p], 1ull) + 1u : 0u;
     probes++;
   }
   for (int off = 32; off > 0; off >>= 1) probes += __shfl_down(probes, off);
   if ((threadIdx.x & 63) == 0 && probes) atomicAdd(&ctr->probes, probes);
 }
 
-// Sender side, after the owners answered: materialise every queued successor
-// whose fingerprint was new at its owner.  The state lives on this shard, next
-// to its parent, so parent pointers (and traces) stay shard-local.
-extern "C" __global__ void k_materialize(Layout L, const uint32_t* __restrict__ cur,
-                                         unsigned long long cur_base,
-                                         const unsigned long long* __restrict__ send_ref,
-                                         const uint8_t* __restrict__ res,
-                                         const unsigned long long* __restrict__ counts, int nshard,
-                                         unsigned long long cap, uint32_t* __restrict__ next,
-                                         unsigned long long* __restrict__ parents,
-                                         unsigned long long next_base, unsigned long long next_cap,
-                                         DevCounters* ctr) {
+// Sender side: materialise the queued successors whose owner answered "new"
+// with a rank in [lo, hi) into the owner's row region (row + parent record,
+// RW = W + 2 words per slot).  Invariants are checked here, where parent and
+// action are known; a violation is recorded against the local parent.
+extern "C" __global__ void k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base,
+                                       int me, const unsigned long long* __restrict__ send_ref,
+                                       const uint32_t* __restrict__ ans,
+                                       const unsigned long long* __restrict__ counts, int nshard,
+                                       unsigned long long cap, unsigned long long lo, unsigned long long hi,
+                                       uint32_t* __restrict__ rows, unsigned long long rows_cap, DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  const int RW = L.W + 2;
   uint32_t all_new[32];
   for (; i < (unsigned long long)nshard * cap; i += stride) {
     unsigned long long p = i / cap, k = i - p * cap;
-    if (k >= counts[p] || !res[i]) continue;
+    if (k >= counts[p]) continue;
+    unsigned long long a = ans[i];
+    if (a == 0 || a - 1 < lo || a - 1 >= hi) continue;
     unsigned long long ref = send_ref[i];
     unsigned long long s = ref >> 16;
     int inst = (int)(ref & 0xffff);
@@ -244,10 +250,11 @@ extern "C" __global__ void k_materialize(Layout L, const uint32_t* __restrict__ 
     compute_delta(L, prow, inst, d);
     FP afp = alllogs_delta(L, prow, all_new);
     FP cfp = fp_add(fp_add(row_fp(prow), afp), delta_fp(L, prow, d));
-    unsigned long long o = atomicAdd(&ctr->next_count, 1ull);
-    if (o >= next_cap) { set_flag(ctr, FLAG_FRONTIER_FULL); continue; }
-    materialize(L, prow, d, all_new, cfp, next + o * (unsigned long long)L.W);
-    parents[next_base + o] = (cur_base + s) << 16 | (unsigned long long)inst;
+    uint32_t* dst = rows + (p * rows_cap + (a - 1 - lo)) * (unsigned long long)RW;
+    materialize(L, prow, d, all_new, cfp, dst);
+    unsigned long long pr = (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
+    dst[L.W] = (uint32_t)pr;
+    dst[L.W + 1] = (uint32_t)(pr >> 32);
     int code = cover_code(L, inst, d.sub);
     atomicAdd(&ctr->cover[COVER_CODES + code], 1ull);
     int bad = check_invariants(L, prow, &d);
@@ -255,8 +262,36 @@ extern "C" __global__ void k_materialize(Layout L, const uint32_t* __restrict__ 
       ctr->viol_parent = cur_base + s;
       ctr->viol_inst = inst;
       ctr->viol_in_model = 1;
-      ctr->viol_child = next_base + o;
+      ctr->viol_child = ~0ull;
     }
+  }
+}
+
+// Owner side: append the received rows to the next frontier (one wave per
+// row, coalesced copy) with their cross-shard parent records.
+extern "C" __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows,
+                                         const unsigned long long* __restrict__ counts, int nshard,
+                                         unsigned long long rows_cap, uint32_t* __restrict__ next,
+                                         unsigned long long* __restrict__ parents, unsigned long long next_base,
+                                         unsigned long long next_cap, DevCounters* ctr) {
+  const int lane = threadIdx.x & 63;
+  const int RW = W + 2;
+  unsigned long long wv = (blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x) >> 6;
+  unsigned long long nw = ((unsigned long long)gridDim.x * blockDim.x) >> 6;
+  for (unsigned long long i = wv; i < (unsigned long long)nshard * rows_cap; i += nw) {
+    unsigned long long p = i / rows_cap, k = i - p * rows_cap;
+    if (k >= counts[p]) continue;
+    const uint32_t* src = rows + i * (unsigned long long)RW;
+    unsigned long long o = 0;
+    if (lane == 0) o = atomicAdd(&ctr->next_count, 1ull);
+    o = shfl0_u64(o);
+    if (o >= next_cap) {
+      if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+      continue;
+    }
+    uint32_t* dst = next + o * (unsigned long long)W;
+    for (int w = lane; w < W; w += 64) dst[w] = src[w];
+    if (lane == 0) parents[next_base + o] = (unsigned long long)src[W] | (unsigned long long)src[W + 1] << 32;
   }
 }
 
@@ -376,26 +411,37 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
 }
 
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
-                                uint64_t* table, int tlog2, uint8_t* res, DevCounters* ctr, hipStream_t st) {
+                                uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
+                                hipStream_t st) {
   uint64_t n = (uint64_t)nshard * cap;
   uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(k_insert_remote, dim3((unsigned)blocks), dim3(256), 0, st,
                      (const unsigned long long*)recv_fp, (const unsigned long long*)counts, nshard,
-                     (unsigned long long)cap, (unsigned long long*)table, tlog2, res, ctr);
+                     (unsigned long long)cap, (unsigned long long*)table, tlog2, ans,
+                     (unsigned long long*)new_count, ctr);
   return hipGetLastError();
 }
 
-hipError_t launch_materialize(const Layout& L, const uint32_t* cur, uint64_t cur_base, const uint64_t* send_ref,
-                              const uint8_t* res, const uint64_t* counts, int nshard, uint64_t cap,
-                              uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
-                              DevCounters* ctr, hipStream_t st) {
+hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+                            const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
+                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, hipStream_t st) {
   uint64_t n = (uint64_t)nshard * cap;
   uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_materialize, dim3((unsigned)blocks), dim3(256), 0, st, L, cur,
-                     (unsigned long long)cur_base, (const unsigned long long*)send_ref, res,
-                     (const unsigned long long*)counts, nshard, (unsigned long long)cap, next,
-                     (unsigned long long*)parents, (unsigned long long)next_base,
-                     (unsigned long long)next_cap, ctr);
+  hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)blocks), dim3(256), 0, st, L, cur, (unsigned long long)cur_base, me,
+                     (const unsigned long long*)send_ref, ans, (const unsigned long long*)counts, nshard,
+                     (unsigned long long)cap, (unsigned long long)lo, (unsigned long long)hi, rows,
+                     (unsigned long long)rows_cap, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, int nshard, uint64_t rows_cap,
+                              uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                              DevCounters* ctr, hipStream_t st) {
+  uint64_t waves = (uint64_t)nshard * rows_cap;
+  uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)blocks), dim3(256), 0, st, W, rows,
+                     (const unsigned long long*)counts, nshard, (unsigned long long)rows_cap, next,
+                     (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap, ctr);
   return hipGetLastError();
 }
 

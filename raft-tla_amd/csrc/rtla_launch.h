@@ -17,9 +17,12 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
                          int grid, hipStream_t st);
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
-                                uint64_t* table, int tlog2, uint8_t* res, DevCounters* ctr, hipStream_t st);
-hipError_t launch_materialize(const Layout& L, const uint32_t* cur, uint64_t cur_base, const uint64_t* send_ref,
-                              const uint8_t* res, const uint64_t* counts, int nshard, uint64_t cap,
+                                uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
+                                hipStream_t st);
+hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+                            const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
+                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, hipStream_t st);
+hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, int nshard, uint64_t rows_cap,
                               uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
                               DevCounters* ctr, hipStream_t st);
 hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
