@@ -172,7 +172,7 @@ extern "C" int rtla_invariants(const rtla_cfg* c, const uint32_t* row) {
   Layout L;
   int r = layout_from_cfg(c, &L);
   if (r) return r;
-  return check_invariants(L, row, (const Delta*)nullptr);
+  return check_invariants<0>(L, row, (const Delta*)nullptr);
 }
 
 extern "C" int rtla_state_text(const rtla_cfg* c, const uint32_t* row, char* buf, size_t cap) {
@@ -485,7 +485,7 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
   }
   HIPCHK(hipStreamSynchronize(x->stream));
   x->level = 1; x->distinct = 1; x->generated = 1; x->inited = true;
-  int bad = check_invariants(L, x->init_row.data(), (const Delta*)nullptr);
+  int bad = check_invariants<0>(L, x->init_row.data(), (const Delta*)nullptr);
   int status = RTLA_OK;
   if (bad) {
     for (auto& s : x->sh)

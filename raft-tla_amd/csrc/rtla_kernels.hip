@@ -2,17 +2,20 @@
 //
 // One BFS level = one launch of k_expand over the current frontier:
 //   * one wavefront per frontier state: the 64 lanes copy the packed row into
-//     LDS (coalesced), lane 0 derives the per-parent allLogs' (raft.tla:465);
+//     LDS (coalesced); lanes 0..N-1 hash the parent's server records and lane
+//     N derives the per-parent allLogs' (raft.tla:465), all into LDS;
 //   * each lane evaluates one action instance of Next (raft.tla:454-463) as a
-//     Delta against the LDS row (rtla_model.h), so every lane reads the same
-//     parent words (LDS broadcast, no bank conflicts);
+//     Delta against the LDS row (rtla_model.h): every lane reads the same
+//     parent words (LDS broadcast, no bank conflicts) and the Delta stays in
+//     VGPRs (the model is instantiated per server count, NS);
 //   * the successor's 128-bit fingerprint is the parent's plus the Delta's
 //     component change (no full re-hash);
 //   * in-model successors probe the open-addressing fingerprint set in HBM
-//     (8-B slots, CAS insert; home slot from fp.a, stored key fp.b | 1);
-//   * new successors are compacted by ballot + popcount prefix, built in an
-//     LDS staging tile (one row per new lane, odd row stride) and written to
-//     the next frontier as one contiguous, coalesced range;
+//     with one 8-byte CAS per probe (home slot from fp.a, key fp.b | 1):
+//     one memory round trip whether the state is new or seen;
+//   * new successors are compacted by ballot + popcount prefix, built in a
+//     16-row LDS staging tile and written to the next frontier as contiguous,
+//     coalesced ranges;
 //   * invariants are checked on every new and every out-of-model successor.
 #include <hip/hip_runtime.h>
 
@@ -24,6 +27,8 @@
 using namespace rtla;
 
 namespace {
+
+constexpr int STAGE_ROWS = 16;  // LDS staging rows per wave
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -37,21 +42,16 @@ __device__ __forceinline__ unsigned long long shfl0_u64(unsigned long long v) {
 }
 
 // Insert into the fingerprint set.  1 = newly inserted, 0 = already present,
-// -1 = probe limit exceeded (set too full).  Slots only ever change 0 -> key,
-// so a plain read that returns a non-zero value is final; a zero is confirmed
-// by the CAS.
+// -1 = probe limit exceeded (set too full).  Slots only ever change 0 -> key;
+// the CAS both tests and claims a slot, so every probe is one round trip.
 __device__ __forceinline__ int fpset_insert(unsigned long long* table, int log2, FP f) {
   const unsigned long long key = f.b | 1ull;
   const unsigned long long mask = (1ull << log2) - 1ull;
   unsigned long long idx = f.a >> (64 - log2);
   for (int probe = 0; probe < 4096; probe++) {
-    unsigned long long cur = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == key) return 0;
-    if (cur == 0ull) {
-      unsigned long long old = atomicCAS(&table[idx], 0ull, key);
-      if (old == 0ull) return 1;
-      if (old == key) return 0;
-    }
+    unsigned long long old = atomicCAS(&table[idx], 0ull, key);
+    if (old == 0ull) return 1;
+    if (old == key) return 0;
     idx = (idx + 1ull) & mask;
   }
   return -1;
@@ -71,27 +71,59 @@ __device__ __forceinline__ int candidate_inst(const Layout& L, int q, int nmsg) 
 
 __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
   int fam = 0;
-  while (fam + 1 < F_COUNT && inst >= L.fam[fam + 1]) fam++;
+#pragma unroll
+  for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
   return fam == F_RECEIVE ? F_COUNT + sub : fam;
+}
+
+// Per-wave LDS: parent row (W) | new allLogs words (32) | parent server-record
+// hashes (NMAX FPs = 4 * NMAX words) | staging rows (STAGE_ROWS * W).
+__host__ __device__ constexpr int wave_lds_words(int W) { return W + 32 + 4 * NMAX + STAGE_ROWS * W; }
+
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  return (unsigned long long)__builtin_amdgcn_readlane((uint32_t)v, l) |
+         (unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32;
+}
+
+// Load the parent row into LDS and derive the per-parent data every lane
+// needs.  Returns the parent fingerprint with allLogs' already applied.
+template <int NS>
+__device__ __forceinline__ FP load_parent(const Layout& L, const uint32_t* __restrict__ src, uint32_t* prow,
+                                          uint32_t* pall, FP* hsrv, int lane) {
+  const int W = L.W;
+  for (int w = lane; w < W; w += 64) prow[w] = src[w];
+  wave_sync();
+  FP afp{0, 0};
+  if (lane < NS) {
+    uint32_t rec[3 + NS];
+    load_rec<NS>(L, prow, lane, rec);
+    hsrv[lane] = h_srv(lane, rec, 3 + NS);
+  } else if (lane == NS) {
+    afp = alllogs_delta<NS>(L, prow, pall);
+  }
+  afp.a = readlane_u64(afp.a, NS);
+  afp.b = readlane_u64(afp.b, NS);
+  wave_sync();
+  return fp_add(row_fp(prow), afp);
 }
 
 }  // namespace
 
-// LDS per wave: parent row (W) + new allLogs words (32) + staging (64 rows x W).
-extern "C" __global__ void __launch_bounds__(256)
+template <int NS>
+__global__ void __launch_bounds__(256)
 k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
-         unsigned long long cur_base, uint32_t* __restrict__ next,
-         unsigned long long* __restrict__ parents, unsigned long long next_base,
-         unsigned long long next_cap, unsigned long long* table, int tlog2, DevCounters* ctr,
-         ShardBox box) {
+         unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
+         unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
+         DevCounters* ctr, ShardBox box) {
   extern __shared__ uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
   const int W = L.W;
-  uint32_t* prow = lds + wave * (W + 32);
+  uint32_t* prow = lds + wave * wave_lds_words(W);
   uint32_t* pall = prow + W;
-  uint32_t* stage = lds + wpb * (W + 32) + wave * 64 * W;
+  FP* hsrv = reinterpret_cast<FP*>(pall + 32);
+  uint32_t* stage = pall + 32 + 4 * NMAX;
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
 
@@ -99,15 +131,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
   const int fixed = L.fam[F_RECEIVE];
   for (unsigned long long s = s_begin + (unsigned long long)blockIdx.x * wpb + wave; s < s_end;
        s += (unsigned long long)gridDim.x * wpb) {
-    const uint32_t* src = cur + s * (unsigned long long)W;
-    for (int w = lane; w < W; w += 64) prow[w] = src[w];
-    wave_sync();
-    FP afp{0, 0};
-    if (lane == 0) afp = alllogs_delta(L, prow, pall);
-    afp.a = shfl0_u64(afp.a);
-    afp.b = shfl0_u64(afp.b);
-    wave_sync();
-    const FP pfp = fp_add(row_fp(prow), afp);
+    const FP pfp = load_parent<NS>(L, cur + s * (unsigned long long)W, prow, pall, hsrv, lane);
     const int nmsg = row_nmsg(L, prow);
     const int ncand = fixed + 3 * nmsg;
     for (int base = 0; base < ncand; base += 64) {
@@ -117,7 +141,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
       int inst = 0;
       if (q < ncand) {
         inst = candidate_inst(L, q, nmsg);
-        compute_delta(L, prow, inst, d);
+        compute_delta<NS>(L, prow, inst, d);
       }
       bool en = d.enabled != 0;
       if (en && d.err) {
@@ -128,7 +152,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
       bool isnew = false;
       FP cfp{0, 0};
       if (en && d.in_model) {
-        cfp = fp_add(pfp, delta_fp(L, prow, d));
+        cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, d.srv >= 0 ? &hsrv[d.srv] : nullptr));
         const int owner = fp_owner(cfp, box.nshard);
         if (owner == box.me) {
           my_probe++;
@@ -137,7 +161,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
           isnew = r == 1;
         } else {
           // Another shard owns this fingerprint: queue (fp, parent, instance);
-          // the owner answers new/seen and this shard materialises the winner.
+          // the owner answers new/seen and this shard ships it the winner.
           unsigned long long slot = atomicAdd(&box.out_count[owner], 1ull);
           if (slot < box.cap) {
             unsigned long long k = (unsigned long long)owner * box.cap + slot;
@@ -162,21 +186,26 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
         rank = __popcll(m & ((1ull << lane) - 1ull));
         if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)cnt);
         obase = shfl0_u64(obase);
-        if (isnew) materialize(L, prow, d, pall, cfp, stage + rank * W);
-        wave_sync();
-        if (obase + cnt <= next_cap) {
-          uint32_t* dst = next + obase * (unsigned long long)W;
-          for (int w = lane; w < cnt * W; w += 64) dst[w] = stage[w];
+        if (obase + cnt > next_cap) {
+          if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+        } else {
+          // stage and write out STAGE_ROWS new rows at a time
+          for (int b = 0; b < cnt; b += STAGE_ROWS) {
+            if (isnew && rank >= b && rank < b + STAGE_ROWS)
+              materialize<NS>(L, prow, d, pall, cfp, stage + (rank - b) * W);
+            wave_sync();
+            const int nb = min(STAGE_ROWS, cnt - b);
+            uint32_t* dst = next + (obase + b) * (unsigned long long)W;
+            for (int w = lane; w < nb * W; w += 64) dst[w] = stage[w];
+            wave_sync();
+          }
           if (isnew)
             parents[next_base + obase + rank] =
                 (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
-        } else if (lane == 0) {
-          set_flag(ctr, FLAG_FRONTIER_FULL);
         }
-        wave_sync();
       }
       if (en && (isnew || !d.in_model)) {
-        int bad = check_invariants(L, prow, &d);
+        int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
         if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
           ctr->viol_parent = cur_base + s;
           ctr->viol_inst = inst;
@@ -186,7 +215,6 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
       }
     }
   }
-  // generated: one atomic per wave
   for (int off = 32; off > 0; off >>= 1) {
     my_gen += __shfl_down(my_gen, off);
     my_probe += __shfl_down(my_probe, off);
@@ -202,11 +230,10 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
 // answer each record with 0 (seen) or 1 + its dense rank among the new
 // fingerprints from that source (the sender uses the rank as the row slot it
 // ships the materialised state into).  Region p holds counts[p] records.
-extern "C" __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
-                                           const unsigned long long* __restrict__ counts, int nshard,
-                                           unsigned long long cap, unsigned long long* table, int tlog2,
-                                           uint32_t* __restrict__ ans, unsigned long long* __restrict__ new_count,
-                                           DevCounters* ctr) {
+__global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
+                                const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
+                                unsigned long long* table, int tlog2, uint32_t* __restrict__ ans,
+                                unsigned long long* __restrict__ new_count, DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   unsigned long long probes = 0;
@@ -227,16 +254,15 @@ extern "C" __global__ void k_insert_remote(const unsigned long long* __restrict_
 // with a rank in [lo, hi) into the owner's row region (row + parent record,
 // RW = W + 2 words per slot).  Invariants are checked here, where parent and
 // action are known; a violation is recorded against the local parent.
-extern "C" __global__ void k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base,
-                                       int me, const unsigned long long* __restrict__ send_ref,
-                                       const uint32_t* __restrict__ ans,
-                                       const unsigned long long* __restrict__ counts, int nshard,
-                                       unsigned long long cap, unsigned long long lo, unsigned long long hi,
-                                       uint32_t* __restrict__ rows, unsigned long long rows_cap, DevCounters* ctr) {
+template <int NS>
+__global__ void k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base, int me,
+                            const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
+                            const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
+                            unsigned long long lo, unsigned long long hi, uint32_t* __restrict__ rows,
+                            unsigned long long rows_cap, DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   const int RW = L.W + 2;
-  uint32_t all_new[32];
   for (; i < (unsigned long long)nshard * cap; i += stride) {
     unsigned long long p = i / cap, k = i - p * cap;
     if (k >= counts[p]) continue;
@@ -247,17 +273,18 @@ extern "C" __global__ void k_pack_rows(Layout L, const uint32_t* __restrict__ cu
     int inst = (int)(ref & 0xffff);
     const uint32_t* prow = cur + s * (unsigned long long)L.W;
     Delta d;
-    compute_delta(L, prow, inst, d);
-    FP afp = alllogs_delta(L, prow, all_new);
-    FP cfp = fp_add(fp_add(row_fp(prow), afp), delta_fp(L, prow, d));
+    compute_delta<NS>(L, prow, inst, d);
     uint32_t* dst = rows + (p * rows_cap + (a - 1 - lo)) * (unsigned long long)RW;
-    materialize(L, prow, d, all_new, cfp, dst);
+    // copy + patch first, then allLogs' straight into the destination row, then the fingerprint
+    materialize<NS>(L, prow, d, prow + L.off_all, FP{0, 0}, dst);
+    FP afp = alllogs_delta<NS>(L, prow, dst + L.off_all);
+    row_set_fp(dst, fp_add(fp_add(row_fp(prow), afp), delta_fp<NS>(L, prow, d)));
     unsigned long long pr = (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
     dst[L.W] = (uint32_t)pr;
     dst[L.W + 1] = (uint32_t)(pr >> 32);
     int code = cover_code(L, inst, d.sub);
     atomicAdd(&ctr->cover[COVER_CODES + code], 1ull);
-    int bad = check_invariants(L, prow, &d);
+    int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
     if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
       ctr->viol_parent = cur_base + s;
       ctr->viol_inst = inst;
@@ -269,11 +296,10 @@ extern "C" __global__ void k_pack_rows(Layout L, const uint32_t* __restrict__ cu
 
 // Owner side: append the received rows to the next frontier (one wave per
 // row, coalesced copy) with their cross-shard parent records.
-extern "C" __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows,
-                                         const unsigned long long* __restrict__ counts, int nshard,
-                                         unsigned long long rows_cap, uint32_t* __restrict__ next,
-                                         unsigned long long* __restrict__ parents, unsigned long long next_base,
-                                         unsigned long long next_cap, DevCounters* ctr) {
+__global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ counts,
+                              int nshard, unsigned long long rows_cap, uint32_t* __restrict__ next,
+                              unsigned long long* __restrict__ parents, unsigned long long next_base,
+                              unsigned long long next_cap, DevCounters* ctr) {
   const int lane = threadIdx.x & 63;
   const int RW = W + 2;
   unsigned long long wv = (blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x) >> 6;
@@ -296,12 +322,11 @@ extern "C" __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ row
 }
 
 // Insert the fingerprints of `n` rows (Init).  new_flags[i] = 1 if new.
-extern "C" __global__ void k_insert_rows(Layout L, const uint32_t* rows, unsigned long long n,
-                                         unsigned long long* table, int tlog2, int* new_flags,
-                                         DevCounters* ctr) {
+__global__ void k_insert_rows(Layout L, const uint32_t* rows, unsigned long long n, unsigned long long* table,
+                              int tlog2, int* new_flags, DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  FP f = row_fp(rows + (unsigned long long)i * L.W);
+  FP f = row_fp(rows + i * (unsigned long long)L.W);
   int r = fpset_insert(table, tlog2, f);
   if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
   new_flags[i] = r == 1;
@@ -309,28 +334,22 @@ extern "C" __global__ void k_insert_rows(Layout L, const uint32_t* rows, unsigne
 
 // Parity seam: every enabled successor of every input row (in-model or not),
 // materialised.  out_info[k] = input index << 32 | in_model << 31 | sub << 16 | inst.
-extern "C" __global__ void __launch_bounds__(256)
-k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n,
-               uint32_t* __restrict__ out, unsigned long long* __restrict__ out_info,
-               unsigned long long cap, DevCounters* ctr) {
+template <int NS>
+__global__ void __launch_bounds__(256)
+k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n, uint32_t* __restrict__ out,
+               unsigned long long* __restrict__ out_info, unsigned long long cap, DevCounters* ctr) {
   extern __shared__ uint32_t lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
   const int W = L.W;
-  uint32_t* prow = lds + wave * (W + 32);
+  uint32_t* prow = lds + wave * wave_lds_words(W);
   uint32_t* pall = prow + W;
-  uint32_t* stage = lds + wpb * (W + 32) + wave * 64 * W;
+  FP* hsrv = reinterpret_cast<FP*>(pall + 32);
+  uint32_t* stage = pall + 32 + 4 * NMAX;
   const int fixed = L.fam[F_RECEIVE];
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wave; s < n;
        s += (unsigned long long)gridDim.x * wpb) {
-    for (int w = lane; w < W; w += 64) prow[w] = rows[s * W + w];
-    wave_sync();
-    FP afp{0, 0};
-    if (lane == 0) afp = alllogs_delta(L, prow, pall);
-    afp.a = shfl0_u64(afp.a);
-    afp.b = shfl0_u64(afp.b);
-    wave_sync();
-    const FP pfp = fp_add(row_fp(prow), afp);
+    const FP pfp = load_parent<NS>(L, rows + s * (unsigned long long)W, prow, pall, hsrv, lane);
     const int nmsg = row_nmsg(L, prow);
     const int ncand = fixed + 3 * nmsg;
     for (int base = 0; base < ncand; base += 64) {
@@ -340,7 +359,7 @@ k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n
       int inst = 0;
       if (q < ncand) {
         inst = candidate_inst(L, q, nmsg);
-        compute_delta(L, prow, inst, d);
+        compute_delta<NS>(L, prow, inst, d);
       }
       bool en = d.enabled != 0;
       if (en && d.err) {
@@ -354,26 +373,30 @@ k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n
       unsigned long long obase = 0;
       if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)cnt);
       obase = shfl0_u64(obase);
-      if (en) materialize(L, prow, d, pall, fp_add(pfp, delta_fp(L, prow, d)), stage + rank * W);
-      wave_sync();
-      if (obase + cnt <= cap) {
-        uint32_t* dst = out + obase * (unsigned long long)W;
-        for (int w = lane; w < cnt * W; w += 64) dst[w] = stage[w];
-        if (en)
-          out_info[obase + rank] = s << 32 | (unsigned long long)(d.in_model ? 1u : 0u) << 31 |
-                                   (unsigned long long)d.sub << 16 | (unsigned long long)inst;
-      } else if (lane == 0) {
-        set_flag(ctr, FLAG_FRONTIER_FULL);
+      if (obase + cnt > cap) {
+        if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+        continue;
       }
-      wave_sync();
+      const FP cfp = en ? fp_add(pfp, delta_fp<NS>(L, prow, d)) : FP{0, 0};
+      for (int b = 0; b < cnt; b += STAGE_ROWS) {
+        if (en && rank >= b && rank < b + STAGE_ROWS) materialize<NS>(L, prow, d, pall, cfp, stage + (rank - b) * W);
+        wave_sync();
+        const int nb = min(STAGE_ROWS, cnt - b);
+        uint32_t* dst = out + (obase + b) * (unsigned long long)W;
+        for (int w = lane; w < nb * W; w += 64) dst[w] = stage[w];
+        wave_sync();
+      }
+      if (en)
+        out_info[obase + rank] = s << 32 | (unsigned long long)(d.in_model ? 1u : 0u) << 31 |
+                                 (unsigned long long)d.sub << 16 | (unsigned long long)inst;
     }
   }
 }
 
 // Microbenchmark kernel: random 8-B CAS inserts into a table (calibrates the
 // random-access roofline of the fingerprint set).
-extern "C" __global__ void k_probe_bench(unsigned long long* table, int tlog2, unsigned long long n,
-                                         unsigned long long seed, DevCounters* ctr) {
+__global__ void k_probe_bench(unsigned long long* table, int tlog2, unsigned long long n, unsigned long long seed,
+                              DevCounters* ctr) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   unsigned long long got = 0;
@@ -389,7 +412,7 @@ extern "C" __global__ void k_probe_bench(unsigned long long* table, int tlog2, u
 namespace rtla {
 
 size_t expand_lds_bytes(const Layout& L, int wpb) {
-  return (size_t)wpb * ((size_t)(L.W + 32) + 64u * (size_t)L.W) * sizeof(uint32_t);
+  return (size_t)wpb * (size_t)wave_lds_words(L.W) * sizeof(uint32_t);
 }
 
 int expand_blocks_per_cu(const Layout& L) {
@@ -398,15 +421,23 @@ int expand_blocks_per_cu(const Layout& L) {
   return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
 
-hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end,
-                         uint64_t cur_base, uint32_t* next, uint64_t* parents, uint64_t next_base,
-                         uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
-                         int grid, hipStream_t st) {
+#define RTLA_DISPATCH_N(L, KERNEL, ...)                        \
+  switch ((L).N) {                                             \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
+  }
+
+hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
+                         uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
+                         int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st) {
   if (s_end <= s_begin) return hipSuccess;
-  hipLaunchKernelGGL(k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
-                     (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base,
-                     next, (unsigned long long*)parents, (unsigned long long)next_base,
-                     (unsigned long long)next_cap, (unsigned long long*)table, tlog2, ctr, box);
+  RTLA_DISPATCH_N(L, k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
+                  (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base, next,
+                  (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,
+                  (unsigned long long*)table, tlog2, ctr, box);
   return hipGetLastError();
 }
 
@@ -415,10 +446,9 @@ hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts,
                                 hipStream_t st) {
   uint64_t n = (uint64_t)nshard * cap;
   uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_insert_remote, dim3((unsigned)blocks), dim3(256), 0, st,
-                     (const unsigned long long*)recv_fp, (const unsigned long long*)counts, nshard,
-                     (unsigned long long)cap, (unsigned long long*)table, tlog2, ans,
-                     (unsigned long long*)new_count, ctr);
+  hipLaunchKernelGGL(k_insert_remote, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned long long*)recv_fp,
+                     (const unsigned long long*)counts, nshard, (unsigned long long)cap, (unsigned long long*)table,
+                     tlog2, ans, (unsigned long long*)new_count, ctr);
   return hipGetLastError();
 }
 
@@ -427,10 +457,10 @@ hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_b
                             uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, hipStream_t st) {
   uint64_t n = (uint64_t)nshard * cap;
   uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)blocks), dim3(256), 0, st, L, cur, (unsigned long long)cur_base, me,
-                     (const unsigned long long*)send_ref, ans, (const unsigned long long*)counts, nshard,
-                     (unsigned long long)cap, (unsigned long long)lo, (unsigned long long)hi, rows,
-                     (unsigned long long)rows_cap, ctr);
+  RTLA_DISPATCH_N(L, k_pack_rows, dim3((unsigned)blocks), dim3(256), 0, st, L, cur, (unsigned long long)cur_base, me,
+                  (const unsigned long long*)send_ref, ans, (const unsigned long long*)counts, nshard,
+                  (unsigned long long)cap, (unsigned long long)lo, (unsigned long long)hi, rows,
+                  (unsigned long long)rows_cap, ctr);
   return hipGetLastError();
 }
 
@@ -445,29 +475,28 @@ hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* count
   return hipGetLastError();
 }
 
-hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
-                              int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st) {
+hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table, int tlog2,
+                              int* new_flags, DevCounters* ctr, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_insert_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, L, rows,
                      (unsigned long long)n, (unsigned long long*)table, tlog2, new_flags, ctr);
   return hipGetLastError();
 }
 
-hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,
-                               uint64_t* info, uint64_t cap, DevCounters* ctr, hipStream_t st) {
+hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out, uint64_t* info,
+                               uint64_t cap, DevCounters* ctr, hipStream_t st) {
   if (n == 0) return hipSuccess;
   uint64_t blocks = (n + 3) / 4;
   int grid = (int)(blocks < 4096 ? blocks : 4096);
-  hipLaunchKernelGGL(k_expand_batch, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, rows,
-                     (unsigned long long)n, out, (unsigned long long*)info, (unsigned long long)cap,
-                     ctr);
+  RTLA_DISPATCH_N(L, k_expand_batch, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, rows,
+                  (unsigned long long)n, out, (unsigned long long*)info, (unsigned long long)cap, ctr);
   return hipGetLastError();
 }
 
-hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed,
-                              DevCounters* ctr, hipStream_t st) {
-  hipLaunchKernelGGL(k_probe_bench, dim3(256 * 16), dim3(256), 0, st, (unsigned long long*)table,
-                     tlog2, (unsigned long long)n, (unsigned long long)seed, ctr);
+hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed, DevCounters* ctr,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(k_probe_bench, dim3(256 * 16), dim3(256), 0, st, (unsigned long long*)table, tlog2,
+                     (unsigned long long)n, (unsigned long long)seed, ctr);
   return hipGetLastError();
 }
 

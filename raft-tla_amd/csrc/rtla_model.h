@@ -320,6 +320,12 @@ RTLA_HD void row_init(const Layout& L, P row) {
 
 // --------------------------------------------------------------- delta ----
 // The successor of one action instance, as a patch of the parent row.
+//
+// Every function below takes the server count as a template parameter NS
+// (0 = read it from the Layout at run time: host-side decoding).  With NS
+// fixed the loops over servers unroll and every array in Delta is indexed
+// with compile-time constants, so the whole Delta stays in VGPRs on the GPU
+// (no scratch); writes at a run-time index go through set_at().
 struct Delta {
   int32_t enabled;
   int32_t in_model;
@@ -327,7 +333,7 @@ struct Delta {
   int32_t err;             // 1: spec evaluation error, 2: row capacity overflow
   int32_t srv;             // server whose record changes, -1 = none
   uint32_t rec[3 + NMAX];  // its new record
-  int32_t nops;            // bag slot writes
+  int32_t nops;            // bag slot writes (<= 3)
   int32_t op_slot[3];
   uint64_t op_old[3], op_new[3];
   int32_t nmsg;            // new number of bag slots in use
@@ -335,27 +341,44 @@ struct Delta {
   uint32_t erec[2 + NMAX];
 };
 
+#define RTLA_NSRV(L) (NS ? NS : (L).N)
+
+// a[j] = v for a run-time j, as a chain of selects (keeps `a` in registers)
+template <int CAP, class T>
+RTLA_HD void set_at(T* a, int j, T v) {
+#pragma unroll
+  for (int k = 0; k < CAP; k++)
+    if (k == j) a[k] = v;
+}
+
 template <class P>
 RTLA_HD uint64_t bag_get(const Layout& L, P row, const Delta& d, int slot) {
-  for (int q = 0; q < d.nops; q++)
-    if (d.op_slot[q] == slot) return d.op_new[q];
-  return bag_slot(L, row, slot);
+  uint64_t v = bag_slot(L, row, slot);
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+    if (q < d.nops && d.op_slot[q] == slot) v = d.op_new[q];
+  return v;
 }
 template <class P>
 RTLA_HD void bag_set(const Layout& L, P row, Delta& d, int slot, uint64_t v) {
-  for (int q = 0; q < d.nops; q++)
-    if (d.op_slot[q] == slot) { d.op_new[q] = v; return; }
+  bool done = false;
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+    if (!done && q < d.nops && d.op_slot[q] == slot) { d.op_new[q] = v; done = true; }
+  if (done) return;
   if (d.nops >= 3) { d.err = 2; return; }
-  d.op_slot[d.nops] = slot;
-  d.op_old[d.nops] = bag_slot(L, row, slot);
-  d.op_new[d.nops] = v;
+  const uint64_t old = bag_slot(L, row, slot);
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+    if (q == d.nops) { d.op_slot[q] = slot; d.op_old[q] = old; d.op_new[q] = v; }
   d.nops++;
 }
 template <class P>
 RTLA_HD int bag_find(const Layout& L, P row, const Delta& d, uint64_t key) {
+  int hit = -1;
   for (int k = 0; k < d.nmsg; k++)
-    if (m_key(bag_get(L, row, d, k)) == key) return k;
-  return -1;
+    if (hit < 0 && m_key(bag_get(L, row, d, k)) == key) hit = k;
+  return hit;
 }
 // raft.tla:106-110 WithMessage
 template <class P>
@@ -385,50 +408,57 @@ RTLA_HD void without_message(const Layout& L, P row, Delta& d, uint64_t key) {
   }
 }
 
-template <class P>
+template <int NS, class P>
 RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
-  for (int w = 0; w < L.SW; w++) rec[w] = row[L.off_srv + i * L.SW + w];
+  const int SW = 3 + RTLA_NSRV(L);
+#pragma unroll
+  for (int w = 0; w < 3 + (NS ? NS : NMAX); w++)
+    if (w < SW) rec[w] = row[L.off_srv + i * SW + w];
 }
 
 // Compute the successor of `row` under action instance `inst` (0..L.fam[F_COUNT]).
 // Follows raft.tla:454-463; allLogs' (:465) is applied per parent by the caller.
-template <class P>
+template <int NS, class P>
 RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
-  const int N = L.N;
+  const int N = RTLA_NSRV(L);
+  const int SW = 3 + N;
   d.enabled = 0; d.in_model = 1; d.sub = R_NONE; d.err = 0; d.srv = -1; d.nops = 0;
   d.nmsg = row_nmsg(L, row); d.elec = 0;
   int fam = 0;
-  while (fam + 1 < F_COUNT && inst >= L.fam[fam + 1]) fam++;
-  int x = inst - L.fam[fam];
+#pragma unroll
+  for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
+  const int x = inst - L.fam[fam];
   uint32_t* rec = d.rec;
 
   if (fam == F_RESTART) {                       // Restart(i) :167-175
-    int i = x;
-    load_rec(L, row, i, rec);
+    const int i = x;
+    load_rec<NS>(L, row, i, rec);
     rec[0] = s_make(s_term(rec[0]), FOLLOWER, s_voted(rec[0]), 0, 0, 0, 0);
     rec[2] = nm_fill(N, 1, 0);
-    for (int j = 0; j < N; j++) rec[3 + j] = 0;
+#pragma unroll
+    for (int j = 0; j < (NS ? NS : NMAX); j++) rec[3 + j] = 0;
     d.srv = i; d.enabled = 1;
   } else if (fam == F_TIMEOUT) {                // Timeout(i) :178-187
-    int i = x;
-    load_rec(L, row, i, rec);
-    uint32_t role = s_role(rec[0]);
+    const int i = x;
+    load_rec<NS>(L, row, i, rec);
+    const uint32_t role = s_role(rec[0]);
     if (role != FOLLOWER && role != CANDIDATE) return;
-    uint32_t t = s_term(rec[0]) + 1;
+    const uint32_t t = s_term(rec[0]) + 1;
     rec[0] = s_make(t, CANDIDATE, NIL, s_commit(rec[0]), 0, 0, 0);
-    for (int j = 0; j < N; j++) rec[3 + j] = 0;
+#pragma unroll
+    for (int j = 0; j < (NS ? NS : NMAX); j++) rec[3 + j] = 0;
     d.srv = i; d.enabled = 1;
     if ((int)t > L.T) d.in_model = 0;
   } else if (fam == F_REQUESTVOTE) {            // RequestVote(i, j) :190-199
-    int i = x / N, j = x % N;
-    uint32_t w0 = row[L.off_srv + i * L.SW], lg = row[L.off_srv + i * L.SW + 1];
+    const int i = x / N, j = x - (x / N) * N;
+    const uint32_t w0 = row[L.off_srv + i * SW], lg = row[L.off_srv + i * SW + 1];
     if (s_role(w0) != CANDIDATE || (s_vresp(w0) >> j & 1u)) return;
     with_message(L, row, d, m_rvreq(i, j, s_term(w0), last_term(lg), log_len(lg)));
     d.enabled = 1;
   } else if (fam == F_BECOMELEADER) {           // BecomeLeader(i) :229-243
-    int i = x;
-    load_rec(L, row, i, rec);
-    uint32_t w0 = rec[0];
+    const int i = x;
+    load_rec<NS>(L, row, i, rec);
+    const uint32_t w0 = rec[0];
     if (s_role(w0) != CANDIDATE) return;
     if (!(__builtin_popcount(s_vgrant(w0)) * 2 > N)) return;   // votesGranted[i] \in Quorum :99
     d.enabled = 1; d.srv = i;
@@ -437,11 +467,16 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
     // elections' = elections \cup {[eterm, eleader, elog, evotes, evoterLog]}
     d.erec[0] = s_term(w0) | (uint32_t)i << 4 | s_vgrant(w0) << 7 | s_vlp(w0) << 12;
     d.erec[1] = rec[1];
-    for (int j = 0; j < N; j++) d.erec[2 + j] = row[L.off_srv + i * L.SW + 3 + j];
-    int ne = row_nelec(L, row), dup = 0;
+#pragma unroll
+    for (int j = 0; j < (NS ? NS : NMAX); j++) d.erec[2 + j] = j < N ? rec[3 + j] : 0u;
+    const int ne = row_nelec(L, row);
+    const int EW = 2 + N;
+    int dup = 0;
     for (int e = 0; e < ne; e++) {
       int same = 1;
-      for (int w = 0; w < L.EW; w++) same &= row[L.off_elec + e * L.EW + w] == d.erec[w];
+#pragma unroll
+      for (int w = 0; w < 2 + (NS ? NS : NMAX); w++)
+        if (w < EW) same &= row[L.off_elec + e * EW + w] == d.erec[w];
       dup |= same;
     }
     if (!dup) {
@@ -449,21 +484,24 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
       d.elec = 1;
     }
   } else if (fam == F_CLIENTREQUEST) {          // ClientRequest(i, v) :246-253
-    int i = x / L.V, v = x % L.V;
-    load_rec(L, row, i, rec);
+    const int i = x / L.V, v = x - (x / L.V) * L.V;
+    load_rec<NS>(L, row, i, rec);
     if (s_role(rec[0]) != LEADER) return;
     if (log_len(rec[1]) >= (uint32_t)LMAX + 1) { d.err = 2; return; }
     rec[1] = log_append(rec[1], s_term(rec[0]) | (uint32_t)v << 3);
     d.srv = i; d.enabled = 1;
     if ((int)log_len(rec[1]) > L.L) d.in_model = 0;
   } else if (fam == F_ADVANCECOMMIT) {          // AdvanceCommitIndex(i) :259-276
-    int i = x;
-    load_rec(L, row, i, rec);
+    const int i = x;
+    load_rec<NS>(L, row, i, rec);
     if (s_role(rec[0]) != LEADER) return;
-    int len = (int)log_len(rec[1]), maxagree = 0;
+    const int len = (int)log_len(rec[1]);
+    int maxagree = 0;
     for (int index = 1; index <= len; index++) {
       int agree = 1;                            // Agree(index) = {i} \cup {k : matchIndex[i][k] >= index}
-      for (int k = 0; k < N; k++) agree += (k != i) && (int)nm_match(rec[2], k) >= index;
+#pragma unroll
+      for (int k = 0; k < (NS ? NS : NMAX); k++)
+        agree += (k < N) && (k != i) && (int)nm_match(rec[2], k) >= index;
       if (agree * 2 > N) maxagree = index;
     }
     uint32_t nci = s_commit(rec[0]);
@@ -471,42 +509,42 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
     rec[0] = (rec[0] & ~(7u << 9)) | nci << 9;
     d.srv = i; d.enabled = 1;
   } else if (fam == F_APPENDENTRIES) {          // AppendEntries(i, j) :204-226
-    int i = x / N, j = x % N;
+    const int i = x / N, j = x - (x / N) * N;
     if (i == j) return;
-    uint32_t w0 = row[L.off_srv + i * L.SW], lg = row[L.off_srv + i * L.SW + 1];
-    uint32_t nm = row[L.off_srv + i * L.SW + 2];
+    const uint32_t w0 = row[L.off_srv + i * SW], lg = row[L.off_srv + i * SW + 1];
+    const uint32_t nm = row[L.off_srv + i * SW + 2];
     if (s_role(w0) != LEADER) return;
-    uint32_t nxt = nm_next(nm, j), prev = nxt - 1, len = log_len(lg);
+    const uint32_t nxt = nm_next(nm, j), prev = nxt - 1, len = log_len(lg);
     uint32_t prevt = 0;
     if (prev > 0) {
       if (prev > len) { d.err = 1; return; }   // log[i][prevLogIndex] outside DOMAIN
       prevt = log_term(lg, prev);
     }
-    uint32_t last = len < nxt ? len : nxt;    // Min({Len(log[i]), nextIndex[i][j]})
-    uint32_t has = nxt <= last ? 1u : 0u;      // SubSeq(log[i], next, lastEntry)
-    uint32_t entry = has ? log_entry(lg, nxt) : 0u;
-    uint32_t ci = s_commit(w0);
-    uint32_t mci = ci < last ? ci : last;
+    const uint32_t last = len < nxt ? len : nxt;   // Min({Len(log[i]), nextIndex[i][j]})
+    const uint32_t has = nxt <= last ? 1u : 0u;     // SubSeq(log[i], next, lastEntry)
+    const uint32_t entry = has ? log_entry(lg, nxt) : 0u;
+    const uint32_t ci = s_commit(w0);
+    const uint32_t mci = ci < last ? ci : last;
     with_message(L, row, d, m_aereq(i, j, s_term(w0), prev, prevt, has, entry, mci, lg));
     d.enabled = 1;
   } else if (fam == F_RECEIVE) {                // Receive(m) :421-436
     if (x >= d.nmsg) return;
-    uint64_t key = m_key(bag_slot(L, row, x));
-    int i = (int)m_dst(key), j = (int)m_src(key);
-    uint32_t mt = m_term(key), type = m_type(key);
-    load_rec(L, row, i, rec);
-    uint32_t cur = s_term(rec[0]), role = s_role(rec[0]);
+    const uint64_t key = m_key(bag_slot(L, row, x));
+    const int i = (int)m_dst(key), j = (int)m_src(key);
+    const uint32_t mt = m_term(key), type = m_type(key);
+    load_rec<NS>(L, row, i, rec);
+    const uint32_t cur = s_term(rec[0]), role = s_role(rec[0]);
     if (mt > cur) {                              // UpdateTerm :406-412 (message kept)
       rec[0] = s_make(mt, FOLLOWER, NIL, s_commit(rec[0]), s_vresp(rec[0]), s_vgrant(rec[0]), s_vlp(rec[0]));
       d.srv = i; d.enabled = 1; d.sub = R_UPDATETERM;
       return;
     }
-    uint32_t lg = rec[1], len = log_len(lg);
+    const uint32_t lg = rec[1], len = log_len(lg);
     if (type == RVREQ) {                         // HandleRequestVoteRequest :284-303
-      uint32_t llt = m_f(key, 12, 4), lli = m_f(key, 16, 3), lt = last_term(lg);
-      int logok = llt > lt || (llt == lt && lli >= len);
-      uint32_t vf = s_voted(rec[0]);
-      int grant = mt == cur && logok && (vf == NIL || vf == (uint32_t)j);
+      const uint32_t llt = m_f(key, 12, 4), lli = m_f(key, 16, 3), lt = last_term(lg);
+      const int logok = llt > lt || (llt == lt && lli >= len);
+      const uint32_t vf = s_voted(rec[0]);
+      const int grant = mt == cur && logok && (vf == NIL || vf == (uint32_t)j);
       if (grant) {
         rec[0] = (rec[0] & ~(7u << 6)) | (uint32_t)j << 6;
         d.srv = i;
@@ -524,27 +562,27 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
           vg |= 1u << j;
           if (!(vlp >> j & 1u)) {                // voterLog[i] @@ (j :> m.mlog): left wins
             vlp |= 1u << j;
-            rec[3 + j] = m_f(key, 16, 28);
+            set_at<NS ? NS : NMAX>(rec + 3, j, m_f(key, 16, 28));
           }
         }
         rec[0] = s_make(cur, role, s_voted(rec[0]), s_commit(rec[0]), vr, vg, vlp);
         without_message(L, row, d, key);
         d.srv = i; d.enabled = 1; d.sub = R_HRVRESP;
       } else {                                   // HandleAppendEntriesResponse :393-403
-        uint32_t succ = m_f(key, 12, 1), mm = m_f(key, 13, 3);
+        const uint32_t succ = m_f(key, 12, 1), mm = m_f(key, 13, 3);
         if (succ) {
           rec[2] = nm_set_match(nm_set_next(rec[2], j, mm + 1), j, mm);
         } else {
-          uint32_t nx = nm_next(rec[2], j);
+          const uint32_t nx = nm_next(rec[2], j);
           rec[2] = nm_set_next(rec[2], j, nx > 2 ? nx - 1 : 1);   // Max({next - 1, 1})
         }
         without_message(L, row, d, key);
         d.srv = i; d.enabled = 1; d.sub = R_HAERESP;
       }
     } else {                                     // HandleAppendEntriesRequest :327-389
-      uint32_t prev = m_f(key, 12, 3), prevt = m_f(key, 15, 4), has = m_f(key, 19, 1);
-      uint32_t entry = m_f(key, 20, 5), mci = m_f(key, 25, 3);
-      int logok = prev == 0 || (prev > 0 && prev <= len && prevt == log_term(lg, prev));
+      const uint32_t prev = m_f(key, 12, 3), prevt = m_f(key, 15, 4), has = m_f(key, 19, 1);
+      const uint32_t entry = m_f(key, 20, 5), mci = m_f(key, 25, 3);
+      const int logok = prev == 0 || (prev > 0 && prev <= len && prevt == log_term(lg, prev));
       if (mt < cur || (mt == cur && role == FOLLOWER && !logok)) {   // reject :333-345
         with_message(L, row, d, m_aeresp(i, j, cur, 0, 0));
         without_message(L, row, d, key);
@@ -553,7 +591,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
         rec[0] = (rec[0] & ~(3u << 4)) | (FOLLOWER << 4);
         d.srv = i; d.enabled = 1; d.sub = R_HAEREQ;
       } else if (mt == cur && role == FOLLOWER && logok) {          // accept :351-388
-        uint32_t index = prev + 1;
+        const uint32_t index = prev + 1;
         if (!has || (len >= index && log_term(lg, index) == (entry & 7u))) {  // already done :356-374
           rec[0] = (rec[0] & ~(7u << 9)) | mci << 9;
           d.srv = i;
@@ -580,19 +618,22 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
     d.enabled = 1;
   }
   if (!d.enabled) return;
-  // State constraint (oracle/MC.tla) on the changed components.
+  // State constraint (specs/MC.tla) on the changed components.
   if (d.srv >= 0) {
     if ((int)s_term(d.rec[0]) > L.T || (int)log_len(d.rec[1]) > L.L) d.in_model = 0;
   }
   if (d.nops) {
     int total_delta = 0;
-    for (int q = 0; q < d.nops; q++) {
-      if ((int)m_count(d.op_new[q]) > L.C) d.in_model = 0;
-      total_delta += (int)m_count(d.op_new[q]) - (int)m_count(d.op_old[q]);
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      if (q < d.nops) {
+        if ((int)m_count(d.op_new[q]) > L.C) d.in_model = 0;
+        total_delta += (int)m_count(d.op_new[q]) - (int)m_count(d.op_old[q]);
+      }
     }
     if (L.M > 0 && total_delta > 0) {
       int total = 0;
-      int nm = row_nmsg(L, row);
+      const int nm = row_nmsg(L, row);
       for (int k = 0; k < nm; k++) total += (int)m_count(bag_slot(L, row, k));
       if (total + total_delta > L.M) d.in_model = 0;
     }
@@ -600,28 +641,39 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
 }
 
 // Fingerprint change of the delta (allLogs change excluded: per parent).
-template <class P>
-RTLA_HD FP delta_fp(const Layout& L, P row, const Delta& d) {
+// `h_old_srv` (optional) = the parent's h_srv of server d.srv, precomputed.
+template <int NS, class P>
+RTLA_HD FP delta_fp(const Layout& L, P row, const Delta& d, const FP* h_old_srv = nullptr) {
+  const int SW = 3 + RTLA_NSRV(L);
   FP f{0, 0};
   if (d.srv >= 0) {
-    uint32_t old[3 + NMAX];
-    load_rec(L, row, d.srv, old);
-    f = fp_sub(h_srv(d.srv, d.rec, L.SW), h_srv(d.srv, old, L.SW));
+    FP old;
+    if (h_old_srv) {
+      old = *h_old_srv;
+    } else {
+      uint32_t orec[3 + NMAX];
+      load_rec<NS>(L, row, d.srv, orec);
+      old = h_srv(d.srv, orec, SW);
+    }
+    f = fp_sub(h_srv(d.srv, d.rec, SW), old);
   }
-  for (int q = 0; q < d.nops; q++) f = fp_add(f, fp_sub(h_msg(d.op_new[q]), h_msg(d.op_old[q])));
-  if (d.elec) f = fp_add(f, h_elec(d.erec, L.EW));
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+    if (q < d.nops) f = fp_add(f, fp_sub(h_msg(d.op_new[q]), h_msg(d.op_old[q])));
+  if (d.elec) f = fp_add(f, h_elec(d.erec, 2 + RTLA_NSRV(L)));
   return f;
 }
 
 // allLogs' = allLogs \cup {log[i] : i \in Server}   (pre-state logs, raft.tla:465)
 // Writes the new allLogs words into all_out and returns the fingerprint change.
-template <class P, class Q>
+template <int NS, class P, class Q>
 RTLA_HD FP alllogs_delta(const Layout& L, P row, Q all_out) {
+  const int N = RTLA_NSRV(L), SW = 3 + N;
   FP f{0, 0};
   for (int w = 0; w < L.all_words; w++) all_out[w] = row[L.off_all + w];
-  for (int i = 0; i < L.N; i++) {
-    int x = log_index(L, row[L.off_srv + i * L.SW + 1]);
-    uint32_t bit = 1u << (x & 31);
+  for (int i = 0; i < N; i++) {
+    const int x = log_index(L, row[L.off_srv + i * SW + 1]);
+    const uint32_t bit = 1u << (x & 31);
     if (!(all_out[x >> 5] & bit)) {
       all_out[x >> 5] |= bit;
       f = fp_add(f, h_all(x));
@@ -632,50 +684,65 @@ RTLA_HD FP alllogs_delta(const Layout& L, P row, Q all_out) {
 
 // Materialise the successor row: child = parent + delta, with new allLogs
 // words and fingerprint.  `child` may alias nothing in `row`.
-template <class P, class Q, class R>
+template <int NS, class P, class Q, class R>
 RTLA_HD void materialize(const Layout& L, P row, const Delta& d, R all_new, FP fp, Q child) {
+  const int SW = 3 + RTLA_NSRV(L), EW = 2 + RTLA_NSRV(L);
   for (int w = 0; w < L.W; w++) child[w] = row[w];
   row_set_fp(child, fp);
-  int ne = row_nelec(L, row) + (d.elec ? 1 : 0);
+  const int ne = row_nelec(L, row) + (d.elec ? 1 : 0);
   child[L.off_hdr] = (uint32_t)d.nmsg | (uint32_t)ne << 8;
-  if (d.srv >= 0)
-    for (int w = 0; w < L.SW; w++) child[L.off_srv + d.srv * L.SW + w] = d.rec[w];
+  if (d.srv >= 0) {
+#pragma unroll
+    for (int w = 0; w < 3 + (NS ? NS : NMAX); w++)
+      if (w < SW) child[L.off_srv + d.srv * SW + w] = d.rec[w];
+  }
   for (int w = 0; w < L.all_words; w++) child[L.off_all + w] = all_new[w];
-  if (d.elec)
-    for (int w = 0; w < L.EW; w++) child[L.off_elec + (ne - 1) * L.EW + w] = d.erec[w];
-  for (int q = 0; q < d.nops; q++) {
-    child[L.off_bag + 2 * d.op_slot[q]] = (uint32_t)d.op_new[q];
-    child[L.off_bag + 2 * d.op_slot[q] + 1] = (uint32_t)(d.op_new[q] >> 32);
+  if (d.elec) {
+#pragma unroll
+    for (int w = 0; w < 2 + (NS ? NS : NMAX); w++)
+      if (w < EW) child[L.off_elec + (ne - 1) * EW + w] = d.erec[w];
+  }
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    if (q < d.nops) {
+      child[L.off_bag + 2 * d.op_slot[q]] = (uint32_t)d.op_new[q];
+      child[L.off_bag + 2 * d.op_slot[q] + 1] = (uint32_t)(d.op_new[q] >> 32);
+    }
   }
 }
 
 // ---------------------------------------------------------- invariants ----
-// Evaluated on the successor (parent + delta) without materialising it.
+// Evaluated on the successor (parent + delta) without materialising it; the
+// delta is passed as the few words the invariants read (srv < 0: none).
 // Returns the mask of VIOLATED invariants among L.inv_mask.
-template <class P>
-RTLA_HD int check_invariants(const Layout& L, P row, const Delta* d) {
-  const int N = L.N;
+template <int NS, class P>
+RTLA_HD int check_invariants_v(const Layout& L, P row, int dsrv, uint32_t drec0, uint32_t drec1, int delec,
+                               uint32_t derec0) {
+  const int N = RTLA_NSRV(L), SW = 3 + N, EW = 2 + N;
+  constexpr int NC = NS ? NS : NMAX;
   int bad = 0;
-  uint32_t w0[NMAX], lg[NMAX];
-  for (int i = 0; i < N; i++) {
-    w0[i] = row[L.off_srv + i * L.SW];
-    lg[i] = row[L.off_srv + i * L.SW + 1];
+  uint32_t w0[NC], lg[NC];
+#pragma unroll
+  for (int i = 0; i < NC; i++) {
+    w0[i] = i < N ? row[L.off_srv + i * SW] : 0u;
+    lg[i] = i < N ? row[L.off_srv + i * SW + 1] : 0u;
+    if (i == dsrv) { w0[i] = drec0; lg[i] = drec1; }
   }
-  if (d && d->srv >= 0) { w0[d->srv] = d->rec[0]; lg[d->srv] = d->rec[1]; }
   if (L.inv_mask & INV_NO_TWO_LEADERS) {
     // NoTwoLeaders == \A i, j \in Server : state[i] = Leader /\ state[j] = Leader => i = j
     int nl = 0;
-    for (int i = 0; i < N; i++) nl += s_role(w0[i]) == LEADER;
+#pragma unroll
+    for (int i = 0; i < NC; i++) nl += (i < N) && s_role(w0[i]) == LEADER;
     if (nl > 1) bad |= INV_NO_TWO_LEADERS;
   }
   if (L.inv_mask & INV_ELECTION_SAFETY) {
     // ElectionSafety == \A e, f \in elections : e.eterm = f.eterm => e.eleader = f.eleader
-    int ne = row_nelec(L, row);
-    int tot = ne + ((d && d->elec) ? 1 : 0);
+    const int ne = row_nelec(L, row);
+    const int tot = ne + (delec ? 1 : 0);
     for (int a = 0; a < tot; a++) {
-      uint32_t ea = a < ne ? row[L.off_elec + a * L.EW] : d->erec[0];
+      const uint32_t ea = a < ne ? row[L.off_elec + a * EW] : derec0;
       for (int b = a + 1; b < tot; b++) {
-        uint32_t eb = b < ne ? row[L.off_elec + b * L.EW] : d->erec[0];
+        const uint32_t eb = b < ne ? row[L.off_elec + b * EW] : derec0;
         if ((ea & 15u) == (eb & 15u) && ((ea >> 4) & 7u) != ((eb >> 4) & 7u)) bad |= INV_ELECTION_SAFETY;
       }
     }
@@ -683,16 +750,26 @@ RTLA_HD int check_invariants(const Layout& L, P row, const Delta* d) {
   if (L.inv_mask & INV_LOG_MATCHING) {
     // LogMatching == \A i, j \in Server : \A n \in 1..Min({Len(log[i]), Len(log[j])}) :
     //   log[i][n].term = log[j][n].term => SubSeq(log[i],1,n) = SubSeq(log[j],1,n)
-    for (int i = 0; i < N; i++)
-      for (int j = i + 1; j < N; j++) {
-        uint32_t a = lg[i], b = lg[j];
-        uint32_t m = log_len(a) < log_len(b) ? log_len(a) : log_len(b);
+#pragma unroll
+    for (int i = 0; i < NC; i++)
+#pragma unroll
+      for (int j = i + 1; j < NC; j++) {
+        if (j >= N) continue;
+        const uint32_t a = lg[i], b = lg[j];
+        const uint32_t m = log_len(a) < log_len(b) ? log_len(a) : log_len(b);
         for (uint32_t n = 1; n <= m; n++)
-          if (log_term(a, n) == log_term(b, n) && log_prefix(a, n) != log_prefix(b, n))
-            bad |= INV_LOG_MATCHING;
+          if (log_term(a, n) == log_term(b, n) && log_prefix(a, n) != log_prefix(b, n)) bad |= INV_LOG_MATCHING;
       }
   }
   return bad;
 }
+
+template <int NS, class P>
+RTLA_HD int check_invariants(const Layout& L, P row, const Delta* d) {
+  if (!d) return check_invariants_v<NS>(L, row, -1, 0u, 0u, 0, 0u);
+  return check_invariants_v<NS>(L, row, d->srv, d->rec[0], d->rec[1], d->elec, d->erec[0]);
+}
+
+#undef RTLA_NSRV
 
 }  // namespace rtla

@@ -217,5 +217,6 @@ def test_virtual_shards_trace():
     assert res.violation == "NoTwoLeaders" and len(res.trace) == g["depth"]
     walk = raft_cpu.Walk(raft_cpu.cfg_of(3, 1, 3, 1, 1, 1, ("NoTwoLeaders",)))
     for label, text in res.trace[1:]:
+        assert text in [t for _, t in walk.successors()], label
         walk.goto(text)
     assert walk.invariants() & 1
