@@ -130,6 +130,9 @@ int rtla_expand_batch(const rtla_cfg *cfg, const uint32_t *rows, size_t n, uint3
 int rtla_state_text(const rtla_cfg *cfg, const uint32_t *row, char *buf, size_t cap);
 int rtla_action_name(const rtla_cfg *cfg, int32_t inst, int32_t sub, char *buf, size_t cap);
 int rtla_invariants(const rtla_cfg *cfg, const uint32_t *row);  /* violated mask */
+/* Fingerprint of a row recomputed from scratch (the kernels derive it
+ * incrementally and store it in the row's first 4 words). */
+int rtla_row_fingerprint(const rtla_cfg *cfg, const uint32_t *row, uint64_t out[2]);
 const char *rtla_strerror(int status);
 int rtla_abi_version(void);
 

@@ -175,6 +175,16 @@ extern "C" int rtla_invariants(const rtla_cfg* c, const uint32_t* row) {
   return check_invariants<0>(L, row, (const Delta*)nullptr);
 }
 
+extern "C" int rtla_row_fingerprint(const rtla_cfg* c, const uint32_t* row, uint64_t out[2]) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  FP f = row_fingerprint(L, row);
+  out[0] = f.a;
+  out[1] = f.b;
+  return RTLA_OK;
+}
+
 extern "C" int rtla_state_text(const rtla_cfg* c, const uint32_t* row, char* buf, size_t cap) {
   Layout L;
   int r = layout_from_cfg(c, &L);

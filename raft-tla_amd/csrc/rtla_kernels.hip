@@ -36,8 +36,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ unsigned long long shfl0_u64(unsigned long long v) {
-  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
   return (unsigned long long)lo | (unsigned long long)hi << 32;
 }
 
@@ -76,13 +76,20 @@ __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
   return fam == F_RECEIVE ? F_COUNT + sub : fam;
 }
 
-// Per-wave LDS: parent row (W) | new allLogs words (32) | parent server-record
-// hashes (NMAX FPs = 4 * NMAX words) | staging rows (STAGE_ROWS * W).
-__host__ __device__ constexpr int wave_lds_words(int W) { return W + 32 + 4 * NMAX + STAGE_ROWS * W; }
+// Per-wave LDS: parent row (W, padded to even) | new allLogs words (32) |
+// parent server-record hashes (NMAX FPs = 4 * NMAX words, 8-byte aligned) |
+// staging rows (STAGE_ROWS * W).  The per-wave block is a multiple of 4
+// words so every wave's hash slots stay 8-byte aligned.
+__host__ __device__ constexpr int even_words(int W) { return (W + 1) & ~1; }
+__host__ __device__ constexpr int wave_lds_words(int W) {
+  return (even_words(W) + 32 + 4 * NMAX + STAGE_ROWS * W + 3) & ~3;
+}
 
+// (the readlane builtins return a signed int: widen through uint32_t)
 __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
-  return (unsigned long long)__builtin_amdgcn_readlane((uint32_t)v, l) |
-         (unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (unsigned long long)lo | (unsigned long long)hi << 32;
 }
 
 // Load the parent row into LDS and derive the per-parent data every lane
@@ -115,13 +122,13 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
          unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
          unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
          DevCounters* ctr, ShardBox box) {
-  extern __shared__ uint32_t lds[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
   const int W = L.W;
   uint32_t* prow = lds + wave * wave_lds_words(W);
-  uint32_t* pall = prow + W;
+  uint32_t* pall = prow + even_words(W);
   FP* hsrv = reinterpret_cast<FP*>(pall + 32);
   uint32_t* stage = pall + 32 + 4 * NMAX;
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
@@ -338,12 +345,12 @@ template <int NS>
 __global__ void __launch_bounds__(256)
 k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n, uint32_t* __restrict__ out,
                unsigned long long* __restrict__ out_info, unsigned long long cap, DevCounters* ctr) {
-  extern __shared__ uint32_t lds[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
   const int W = L.W;
   uint32_t* prow = lds + wave * wave_lds_words(W);
-  uint32_t* pall = prow + W;
+  uint32_t* pall = prow + even_words(W);
   FP* hsrv = reinterpret_cast<FP*>(pall + 32);
   uint32_t* stage = pall + 32 + 4 * NMAX;
   const int fixed = L.fam[F_RECEIVE];

@@ -78,6 +78,7 @@ def _load():
         "rtla_state_text": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_char_p, C.c_size_t]),
         "rtla_action_name": (C.c_int, [P(_Cfg), C.c_int32, C.c_int32, C.c_char_p, C.c_size_t]),
         "rtla_invariants": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
+        "rtla_row_fingerprint": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_uint64)]),
         "rtla_strerror": (C.c_char_p, [C.c_int]),
         "rtla_abi_version": (C.c_int, []),
         "rtla_comm_id": (C.c_int, [C.c_void_p]),
@@ -94,7 +95,7 @@ _lib = _load()
 
 EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset", "rtla_step", "rtla_violation",
             "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
-            "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants",
+            "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench"]
 
 
@@ -198,6 +199,19 @@ def invariants_violated(cfg: Config, row: Sequence[int]) -> int:
     cc = cfg.c()
     arr = (C.c_uint32 * len(row))(*row)
     return _check(_lib.rtla_invariants(C.byref(cc), arr), "rtla_invariants")
+
+
+def row_fingerprint(cfg: Config, row: Sequence[int]):
+    """(a, b) recomputed from scratch; the row stores the incrementally derived one in words 0-3."""
+    cc = cfg.c()
+    arr = (C.c_uint32 * len(row))(*row)
+    out = (C.c_uint64 * 2)()
+    _check(_lib.rtla_row_fingerprint(C.byref(cc), arr, out), "rtla_row_fingerprint")
+    return out[0], out[1]
+
+
+def stored_fingerprint(row: Sequence[int]):
+    return row[0] | row[1] << 32, row[2] | row[3] << 32
 
 
 def expand_batch(cfg: Config, rows: Sequence[Sequence[int]]):

@@ -220,3 +220,24 @@ def test_virtual_shards_trace():
         assert text in [t for _, t in walk.successors()], label
         walk.goto(text)
     assert walk.invariants() & 1
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_stored_fingerprints_equal_full_rehash(shards):
+    """Every row the search stores carries the fingerprint derived
+    incrementally from its parent; it must equal a from-scratch hash of the
+    row (a wrong stored fingerprint silently breaks dedup at the next level)."""
+    g = GOLD["n2_v2_t3_l2_m1"]
+    kw = small_kw(g)
+    kw["mem_budget"] *= shards
+    cfg = cfg_of(g, shards=shards, chunk=512, **kw)
+    with rtla.Checker(cfg) as ck:
+        st = ck.init()
+        level = 1
+        while st == rtla.OK and level < 16:
+            st = ck.step()
+            level += 1
+            rows = ck.frontier()
+            bad = [r for r in rows if rtla.stored_fingerprint(r) != rtla.row_fingerprint(cfg, r)]
+            assert not bad, "level %d: %d of %d rows carry a wrong fingerprint; first:\n%s" % (
+                level, len(bad), len(rows), rtla.state_text(cfg, bad[0]))
