@@ -233,6 +233,267 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
+// ------------------------------------------------------------------------
+// k_expand_lane: the BFS level kernel, one LANE per frontier state.
+//
+// A wave takes 64 consecutive frontier rows (one coalesced copy into LDS,
+// odd row stride W so lane-strided reads hit 64 distinct banks) and walks the
+// action-instance space q = 0..ncand-1 in lock-step: every lane evaluates the
+// SAME instance on its own state, so the family dispatch in compute_delta is a
+// uniform (scalar) branch and the wave never diverges across Next's
+// disjuncts.  Bag instances (Receive / Duplicate / Drop of slot k) run for
+// k < the wave's largest bag; lanes with fewer messages are simply disabled.
+//
+// Phase 1 (per chunk of 64 instances): delta, incremental fingerprint, one
+// CAS probe of the fingerprint set per in-model successor (skipped when the
+// successor equals its parent, which is already in the set), invariants on
+// new and out-of-model successors, coverage; new / remote successors are
+// remembered as one bit per (lane, instance).
+// Phase 2: ONE atomic reserves the whole wave's new rows (and one per
+// remote owner its records), then the flagged instances are re-derived and
+// materialised straight into the next frontier.  The reservation atomics
+// drop from one per state to one per 64 states: a single counter word
+// saturates at ~9e7 atomics/s on MI355X.
+namespace {
+
+struct LaneWords {  // word w of a per-lane array kept word-major (stride 64: bank-conflict free)
+  uint32_t* p;
+  __device__ __forceinline__ uint32_t& operator[](int w) const { return p[w * 64]; }
+};
+
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo |= (uint32_t)__shfl_xor((int)lo, o);
+    hi |= (uint32_t)__shfl_xor((int)hi, o);
+  }
+  return (unsigned long long)lo | (unsigned long long)hi << 32;
+}
+// exclusive prefix sum over the wave; *total = the wave's sum (uniform)
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  *total = __builtin_amdgcn_readlane(x, 63);
+  return x - v;
+}
+
+// q-th candidate of the wave -> instance id (uniform); *slot = bag slot or -1
+__device__ __forceinline__ int wave_inst(const Layout& L, int q, int fixed, int kmax) {
+  if (q < fixed) return q;
+  const int r = q - fixed, fam = r / kmax;
+  return L.fam[F_RECEIVE + fam] + (r - fam * kmax);
+}
+
+template <int NS>
+__device__ __forceinline__ FP sel_fp(const FP* h, int i) {
+  FP r{0, 0};
+#pragma unroll
+  for (int k = 0; k < NS; k++)
+    if (k == i) r = h[k];
+  return r;
+}
+
+__host__ __device__ constexpr int lane_lds_words(int W, int AW) { return 64 * W + 64 * AW; }
+
+}  // namespace
+
+template <int NS, bool MULTI>
+__global__ void __launch_bounds__(256)
+k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
+              unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
+              unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
+              DevCounters* ctr, ShardBox box) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ unsigned int cov[2 * COVER_CODES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int W = L.W, AW = L.all_words;
+  uint32_t* rows = lds + wave * lane_lds_words(W, AW);
+  const uint32_t* prow = rows + lane * W;
+  const LaneWords pall{rows + 64 * W + lane};
+  for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
+  __syncthreads();
+
+  unsigned long long my_gen = 0, my_probe = 0;
+  const int fixed = L.fam[F_RECEIVE];
+  const int G = MULTI ? box.nshard : 1;
+  for (unsigned long long s0 = s_begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; s0 < s_end;
+       s0 += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const int nvalid = (int)min<unsigned long long>(64ull, s_end - s0);
+    {  // coalesced copy of the group's rows
+      const uint32_t* src = cur + s0 * (unsigned long long)W;
+      const int nw = nvalid * W;
+      for (int w = lane; w < nw; w += 64) rows[w] = src[w];
+    }
+    wave_sync();
+    const bool valid = lane < nvalid;
+    const unsigned long long s = s0 + lane;  // this lane's state
+    FP hs[NS];
+    FP pfp0{0, 0}, pfp{0, 0};
+    int nmsg = 0;
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < NS; i++) {
+        uint32_t rec[3 + NS];
+        load_rec<NS>(L, prow, i, rec);
+        hs[i] = h_srv(i, rec, 3 + NS);
+      }
+      pfp0 = row_fp(prow);
+      pfp = fp_add(pfp0, alllogs_delta<NS>(L, prow, pall));
+      nmsg = row_nmsg(L, prow);
+    }
+    const int kmax = wave_max_i(nmsg);
+    const int ncand = fixed + 3 * kmax;
+    for (int base = 0; base < ncand; base += 64) {
+      const int qend = min(ncand, base + 64);
+      unsigned long long newm = 0, remm = 0;
+      int rcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      // ---- phase 1: evaluate, probe, check
+      for (int q = base; q < qend; q++) {
+        const int inst = wave_inst(L, q, fixed, kmax);
+        Delta d;
+        d.enabled = 0;
+        if (valid) compute_delta<NS>(L, prow, inst, d);
+        bool en = d.enabled != 0;
+        if (en && d.err) {
+          set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
+          en = false;
+        }
+        my_gen += en ? 1 : 0;
+        bool isnew = false;
+        if (en && d.in_model) {
+          const FP hold = sel_fp<NS>(hs, d.srv);
+          const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, &hold));
+          if (cfp.a != pfp0.a || cfp.b != pfp0.b) {  // successor == parent: already in the set
+            const int owner = MULTI ? fp_owner(cfp, G) : 0;
+            if (!MULTI || owner == box.me) {
+              my_probe++;
+              const int r = fpset_insert(table, tlog2, cfp);
+              if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
+              isnew = r == 1;
+              if (isnew) newm |= 1ull << (q - base);
+            } else {
+              remm |= 1ull << (q - base);
+#pragma unroll
+              for (int o = 0; o < 8; o++) rcnt[o] += o == owner;
+            }
+          }
+        }
+        // coverage: the family is uniform; Receive's sub-action is per lane
+        if (q < fixed || (q - fixed) / kmax != 0) {
+          const int code = cover_code(L, inst, R_NONE);
+          const int c1 = __popcll(__ballot(en)), c2 = __popcll(__ballot(isnew));
+          if (lane == 0) {
+            if (c1) atomicAdd(&cov[code], (unsigned)c1);
+            if (c2) atomicAdd(&cov[COVER_CODES + code], (unsigned)c2);
+          }
+        } else {
+#pragma unroll
+          for (int sub = 0; sub < R_NONE; sub++) {
+            const int c1 = __popcll(__ballot(en && d.sub == sub)), c2 = __popcll(__ballot(isnew && d.sub == sub));
+            if (lane == 0) {
+              if (c1) atomicAdd(&cov[F_COUNT + sub], (unsigned)c1);
+              if (c2) atomicAdd(&cov[COVER_CODES + F_COUNT + sub], (unsigned)c2);
+            }
+          }
+        }
+        if (en && (isnew || !d.in_model)) {
+          const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+          if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+            ctr->viol_parent = cur_base + s;
+            ctr->viol_inst = inst;
+            ctr->viol_in_model = d.in_model;
+            ctr->viol_child = ~0ull;
+          }
+        }
+      }
+      // ---- phase 2: reserve, then materialise the flagged successors
+      int total = 0;
+      const int mine = __popcll(newm);
+      const int off = wave_excl_scan(mine, lane, &total);
+      unsigned long long obase = 0;
+      bool write_new = false;
+      if (total) {
+        if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)total);
+        obase = shfl0_u64(obase);
+        write_new = obase + total <= next_cap;
+        if (!write_new && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+      }
+      unsigned long long robase[8];
+      int roff[8];
+      bool any_rem = false;
+      if (MULTI) {
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+          int tot = 0;
+          roff[o] = o < G ? wave_excl_scan(rcnt[o], lane, &tot) : 0;
+          unsigned long long b = 0;
+          if (tot) {
+            any_rem = true;
+            if (lane == 0) b = atomicAdd(&box.out_count[o], (unsigned long long)tot);
+            b = shfl0_u64(b);
+          }
+          robase[o] = b;
+        }
+      }
+      unsigned long long todo = (write_new ? wave_or_u64(newm) : 0ull) | (any_rem ? wave_or_u64(remm) : 0ull);
+      int k_new = 0;
+      while (todo) {
+        const int bit = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const bool want_new = write_new && (newm >> bit & 1ull);
+        const bool want_rem = any_rem && (remm >> bit & 1ull);
+        if (!(want_new || want_rem)) continue;
+        const int inst = wave_inst(L, base + bit, fixed, kmax);
+        Delta d;
+        compute_delta<NS>(L, prow, inst, d);
+        const FP hold = sel_fp<NS>(hs, d.srv);
+        const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, &hold));
+        if (want_new) {
+          const unsigned long long slot = obase + off + k_new++;
+          materialize<NS>(L, prow, d, pall, cfp, next + slot * (unsigned long long)W);
+          parents[next_base + slot] =
+              (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
+        } else {
+          const int owner = fp_owner(cfp, G);
+          unsigned long long slot = 0;
+#pragma unroll
+          for (int o = 0; o < 8; o++)
+            if (o == owner) slot = robase[o] + (unsigned long long)roff[o]++;
+          if (slot < box.cap) {
+            const unsigned long long k = (unsigned long long)owner * box.cap + slot;
+            box.send_fp[2 * k] = cfp.a;
+            box.send_fp[2 * k + 1] = cfp.b;
+            box.send_ref[k] = s << 16 | (unsigned long long)inst;
+          } else {
+            set_flag(ctr, FLAG_OUTBOX_FULL);
+          }
+        }
+      }
+    }
+    wave_sync();  // the next group overwrites this group's rows
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    my_gen += __shfl_down(my_gen, off);
+    my_probe += __shfl_down(my_probe, off);
+  }
+  if (lane == 0 && my_gen) atomicAdd(&ctr->generated, my_gen);
+  if (lane == 0 && my_probe) atomicAdd(&ctr->probes, my_probe);
+  __syncthreads();
+  for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x)
+    if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
+}
+
 // Owner side of the exchange: insert the fingerprints other shards sent and
 // answer each record with 0 (seen) or 1 + its dense rank among the new
 // fingerprints from that source (the sender uses the rank as the row slot it
@@ -422,6 +683,12 @@ size_t expand_lds_bytes(const Layout& L, int wpb) {
   return (size_t)wpb * (size_t)wave_lds_words(L.W) * sizeof(uint32_t);
 }
 
+int expand_lane_wpb(const Layout& L) {
+  const size_t per = (size_t)lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+  if (per > 64 * 1024) return 0;
+  return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
+}
+
 int expand_blocks_per_cu(const Layout& L) {
   size_t per = expand_lds_bytes(L, 4) + 2 * COVER_CODES * sizeof(unsigned int);
   int b = (int)((160u * 1024u) / per);
@@ -441,6 +708,31 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
                          uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
                          int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st) {
   if (s_end <= s_begin) return hipSuccess;
+  const int wpb = expand_lane_wpb(L);
+  if (wpb > 0) {  // one lane per state (rows fit LDS)
+    const uint64_t groups = (s_end - s_begin + 63) / 64;
+    const uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
+    const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+    const bool multi = box.nshard > 1;
+#define RTLA_LANE_CASE(n)                                                                                     \
+  case n: {                                                                                                   \
+    auto kfn = multi ? k_expand_lane<n, true> : k_expand_lane<n, false>;                                      \
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)s_begin, \
+                       (unsigned long long)s_end, (unsigned long long)cur_base, next, (unsigned long long*)parents, \
+                       (unsigned long long)next_base, (unsigned long long)next_cap, (unsigned long long*)table,  \
+                       tlog2, ctr, box);                                                                      \
+  } break;
+    switch (L.N) {
+      RTLA_LANE_CASE(1)
+      RTLA_LANE_CASE(2)
+      RTLA_LANE_CASE(3)
+      RTLA_LANE_CASE(4)
+      default: RTLA_LANE_CASE(5)
+    }
+#undef RTLA_LANE_CASE
+    return hipGetLastError();
+  }
+  // rows too wide for 64 per wave in LDS: one wave per state
   RTLA_DISPATCH_N(L, k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
                   (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base, next,
                   (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,

@@ -9,6 +9,9 @@ namespace rtla {
 
 // LDS bytes a k_expand / k_expand_batch block of `wpb` waves needs.
 size_t expand_lds_bytes(const Layout& L, int wpb);
+// Waves per block of the lane-per-state k_expand_lane (0: rows too wide,
+// the wave-per-state k_expand is used).
+int expand_lane_wpb(const Layout& L);
 // Blocks of 4 waves that fit on one CU given the LDS footprint.
 int expand_blocks_per_cu(const Layout& L);
 

@@ -13,8 +13,8 @@ step() {  # name, limit, cmd...
   local rc=$?; echo "   rc=$rc"; tail -5 "$OUT/$name.log"
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-[ "${SKIP_TESTS:-0}" = 1 ] || step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+[ "${SKIP_TESTS:-0}" = 1 ] || step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"}
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --levels
-step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- python bench.py --steps 2 --warmup 1 --no-cpu --workload "$W"
+[ "${SKIP_TRACE:-0}" = 1 ] || step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- python bench.py --steps 2 --warmup 1 --no-cpu --workload "$W"
 echo done
