@@ -35,6 +35,9 @@ WORKLOADS = {
 }
 DEFAULT = "raft3_v2_t2_l1_m2"
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+# Random 8-B CAS into a table far beyond the 256 MiB Infinity Cache, all CUs:
+# measured on MI355X by tools/probe_calib.py (profiles/).
+CAS_CEILING_PER_S = 2.0e10
 
 
 def dist_env():
@@ -64,6 +67,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=12_000_000, help="states in the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--fpset-log2", type=int, default=30,
+                    help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 2^30 x 8 B = 8 GiB "
+                         "holds the bench model at 14%% load. 0 = auto (40%% of free HBM)")
     ap.add_argument("--levels", action="store_true", help="print the per-level table to stderr")
     args = ap.parse_args()
 
@@ -81,7 +87,7 @@ def main():
 
     shape = WORKLOADS[args.workload]
     n, v, t, l, c, m, inv = shape
-    cfg = rtla.Config(n, v, t, l, c, m, inv)
+    cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=args.fpset_log2)
     ck = rtla.Checker(cfg, rank=rank, world=world, comm_id=comm_id)
 
     def barrier():
@@ -153,6 +159,7 @@ def main():
             "servers": n, "values": v, "max_term": t, "max_log": l, "max_copies": c, "max_in_flight": m,
             "invariants": list(inv), "distinct": distinct, "generated": generated, "depth": depth,
             "parallelism": "single" if world == 1 else "fp-sharded%d" % world,
+            "fpset_slots_log2": args.fpset_log2,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -162,6 +169,9 @@ def main():
             "algorithmic_bytes": stream_bytes + probe_bytes,
             "model": "E*S + D*(S+8) streamed + one 64-B transaction per fingerprint probe",
             "probes_per_s": P / (kms / 1e3),
+            "random_access": {"probes_per_s": P / (kms / 1e3), "ceiling_per_s": CAS_CEILING_PER_S,
+                              "frac": P / (kms / 1e3) / CAS_CEILING_PER_S,
+                              "source": "tools/probe_calib.py (random 8-B CAS, 8-32 GiB tables)"},
         },
         "cpu_baseline": None,
     }

@@ -47,6 +47,7 @@ struct DevCounters {
   int viol_in_model;
   unsigned long long viol_parent;
   unsigned long long viol_child;
+  unsigned long long mat_begin;  // k_materialize: first next-frontier slot of the current expand launch
   unsigned long long cover[2 * COVER_CODES];  // [0,C): generated, [C,2C): distinct
 };
 

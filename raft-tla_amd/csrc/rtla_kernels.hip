@@ -59,6 +59,22 @@ __device__ __forceinline__ int fpset_insert(unsigned long long* table, int log2,
 
 __device__ __forceinline__ void set_flag(DevCounters* c, int f) { atomicOr(&c->flags, f); }
 
+// Finish an insert whose first CAS (at home slot `idx`) returned `old`:
+// continue linear probing while the slot holds another key.  true = new.
+__device__ __forceinline__ bool fpset_resolve(unsigned long long* table, int log2, unsigned long long key,
+                                              unsigned long long idx, unsigned long long old, DevCounters* ctr) {
+  const unsigned long long mask = (1ull << log2) - 1ull;
+  for (int probe = 1; old != 0ull && old != key; probe++) {
+    if (probe >= 4096) {
+      set_flag(ctr, FLAG_FPSET_FULL);
+      return false;
+    }
+    idx = (idx + 1ull) & mask;
+    old = atomicCAS(&table[idx], 0ull, key);
+  }
+  return old == 0ull;
+}
+
 // Map the q-th candidate of a parent with `nmsg` bag slots to an instance id:
 // the fixed families first, then Receive / Duplicate / Drop over used slots.
 __device__ __forceinline__ int candidate_inst(const Layout& L, int q, int nmsg) {
@@ -307,8 +323,11 @@ __host__ __device__ constexpr int lane_lds_words(int W, int AW) { return 64 * W 
 
 }  // namespace
 
+#ifndef RTLA_LANE_WAVES_PER_EU
+#define RTLA_LANE_WAVES_PER_EU 1
+#endif
 template <int NS, bool MULTI>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_LANE_WAVES_PER_EU)))
 k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
               unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
               unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
@@ -324,7 +343,7 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
 
-  unsigned long long my_gen = 0, my_probe = 0;
+  unsigned my_gen = 0, my_probe = 0;
   const int fixed = L.fam[F_RECEIVE];
   const int G = MULTI ? box.nshard : 1;
   for (unsigned long long s0 = s_begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; s0 < s_end;
@@ -338,16 +357,9 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
     wave_sync();
     const bool valid = lane < nvalid;
     const unsigned long long s = s0 + lane;  // this lane's state
-    FP hs[NS];
     FP pfp0{0, 0}, pfp{0, 0};
     int nmsg = 0;
     if (valid) {
-#pragma unroll
-      for (int i = 0; i < NS; i++) {
-        uint32_t rec[3 + NS];
-        load_rec<NS>(L, prow, i, rec);
-        hs[i] = h_srv(i, rec, 3 + NS);
-      }
       pfp0 = row_fp(prow);
       pfp = fp_add(pfp0, alllogs_delta<NS>(L, prow, pall));
       nmsg = row_nmsg(L, prow);
@@ -358,10 +370,15 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
       const int qend = min(ncand, base + 64);
       unsigned long long newm = 0, remm = 0;
       int rcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      // ---- phase 1: evaluate, probe, check
+      // ---- phase 1: evaluate and probe.  The CAS of instance q is resolved
+      // only after instance q+1's delta and fingerprint are computed, so
+      // every wave keeps one probe in flight behind its own arithmetic.
+      bool pend = false;
+      unsigned long long pold = 0, pkey = 0, pidx = 0;
+      int pbit = 0;
       for (int q = base; q < qend; q++) {
         const int inst = wave_inst(L, q, fixed, kmax);
-        Delta d;
+        DeltaFp d;
         d.enabled = 0;
         if (valid) compute_delta<NS>(L, prow, inst, d);
         bool en = d.enabled != 0;
@@ -370,18 +387,16 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
           en = false;
         }
         my_gen += en ? 1 : 0;
-        bool isnew = false;
+        bool probe = false;
+        unsigned long long key = 0, idx = 0;
         if (en && d.in_model) {
-          const FP hold = sel_fp<NS>(hs, d.srv);
-          const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, &hold));
+          const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
           if (cfp.a != pfp0.a || cfp.b != pfp0.b) {  // successor == parent: already in the set
             const int owner = MULTI ? fp_owner(cfp, G) : 0;
             if (!MULTI || owner == box.me) {
-              my_probe++;
-              const int r = fpset_insert(table, tlog2, cfp);
-              if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
-              isnew = r == 1;
-              if (isnew) newm |= 1ull << (q - base);
+              probe = true;
+              key = cfp.b | 1ull;
+              idx = cfp.a >> (64 - tlog2);
             } else {
               remm |= 1ull << (q - base);
 #pragma unroll
@@ -389,33 +404,43 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
             }
           }
         }
-        // coverage: the family is uniform; Receive's sub-action is per lane
+        // generated coverage: the family is uniform; Receive's sub-action is per lane
+#ifdef RTLA_EXP_NOCOV
+        if (0)
+#endif
         if (q < fixed || (q - fixed) / kmax != 0) {
-          const int code = cover_code(L, inst, R_NONE);
-          const int c1 = __popcll(__ballot(en)), c2 = __popcll(__ballot(isnew));
-          if (lane == 0) {
-            if (c1) atomicAdd(&cov[code], (unsigned)c1);
-            if (c2) atomicAdd(&cov[COVER_CODES + code], (unsigned)c2);
-          }
+          const int c1 = __popcll(__ballot(en));
+          if (lane == 0 && c1) atomicAdd(&cov[cover_code(L, inst, R_NONE)], (unsigned)c1);
         } else {
 #pragma unroll
           for (int sub = 0; sub < R_NONE; sub++) {
-            const int c1 = __popcll(__ballot(en && d.sub == sub)), c2 = __popcll(__ballot(isnew && d.sub == sub));
-            if (lane == 0) {
-              if (c1) atomicAdd(&cov[F_COUNT + sub], (unsigned)c1);
-              if (c2) atomicAdd(&cov[COVER_CODES + F_COUNT + sub], (unsigned)c2);
-            }
+            const int c1 = __popcll(__ballot(en && d.sub == sub));
+            if (lane == 0 && c1) atomicAdd(&cov[F_COUNT + sub], (unsigned)c1);
           }
         }
-        if (en && (isnew || !d.in_model)) {
+        if (en && !d.in_model) {  // out-of-model successors: checked, never stored
           const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
           if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
             ctr->viol_parent = cur_base + s;
             ctr->viol_inst = inst;
-            ctr->viol_in_model = d.in_model;
+            ctr->viol_in_model = 0;
             ctr->viol_child = ~0ull;
           }
         }
+        if (pend) {
+          if (fpset_resolve(table, tlog2, pkey, pidx, pold, ctr)) newm |= 1ull << pbit;
+        }
+        pend = probe;
+        if (probe) {
+          my_probe++;
+          pkey = key;
+          pidx = idx;
+          pbit = q - base;
+          pold = atomicCAS(&table[idx], 0ull, key);
+        }
+      }
+      if (pend) {
+        if (fpset_resolve(table, tlog2, pkey, pidx, pold, ctr)) newm |= 1ull << pbit;
       }
       // ---- phase 2: reserve, then materialise the flagged successors
       int total = 0;
@@ -446,25 +471,31 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
           robase[o] = b;
         }
       }
-      unsigned long long todo = (write_new ? wave_or_u64(newm) : 0ull) | (any_rem ? wave_or_u64(remm) : 0ull);
-      int k_new = 0;
-      while (todo) {
-        const int bit = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        const bool want_new = write_new && (newm >> bit & 1ull);
-        const bool want_rem = any_rem && (remm >> bit & 1ull);
-        if (!(want_new || want_rem)) continue;
-        const int inst = wave_inst(L, base + bit, fixed, kmax);
-        Delta d;
-        compute_delta<NS>(L, prow, inst, d);
-        const FP hold = sel_fp<NS>(hs, d.srv);
-        const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, &hold));
-        if (want_new) {
-          const unsigned long long slot = obase + off + k_new++;
-          materialize<NS>(L, prow, d, pall, cfp, next + slot * (unsigned long long)W);
-          parents[next_base + slot] =
-              (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
-        } else {
+      // local new successors: only the parent record is written here;
+      // k_materialize builds the rows (its own launch, its own registers)
+      if (write_new) {
+        unsigned long long todo = wave_or_u64(newm);
+        int k_new = 0;
+        while (todo) {
+          const int bit = __builtin_ctzll(todo);
+          todo &= todo - 1;
+          if (newm >> bit & 1ull) {
+            const int inst = wave_inst(L, base + bit, fixed, kmax);
+            parents[next_base + obase + off + k_new++] =
+                (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
+          }
+        }
+      }
+      if (MULTI && any_rem) {  // successors owned by other shards: (fp, parent ref) records
+        unsigned long long todo = wave_or_u64(remm);
+        while (todo) {
+          const int bit = __builtin_ctzll(todo);
+          todo &= todo - 1;
+          if (!(remm >> bit & 1ull)) continue;
+          const int inst = wave_inst(L, base + bit, fixed, kmax);
+          DeltaFp d;
+          compute_delta<NS>(L, prow, inst, d);
+          const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
           const int owner = fp_owner(cfp, G);
           unsigned long long slot = 0;
 #pragma unroll
@@ -487,11 +518,63 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
     my_gen += __shfl_down(my_gen, off);
     my_probe += __shfl_down(my_probe, off);
   }
-  if (lane == 0 && my_gen) atomicAdd(&ctr->generated, my_gen);
-  if (lane == 0 && my_probe) atomicAdd(&ctr->probes, my_probe);
+  if (lane == 0 && my_gen) atomicAdd(&ctr->generated, (unsigned long long)my_gen);
+  if (lane == 0 && my_probe) atomicAdd(&ctr->probes, (unsigned long long)my_probe);
   __syncthreads();
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x)
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
+}
+
+// k_materialize: build the rows of the new states k_expand_lane found.
+// Slots [ctr->mat_begin, ctr->next_count) of the next frontier hold only a
+// parent record (shard << 56 | parent index << 16 | action instance); one
+// lane per slot stages its parent row in LDS, re-derives the successor with
+// the full Delta, writes the row with its fingerprint, checks the invariants
+// (raft.cfg:3, specs/MC.tla) and counts the distinct coverage.
+template <int NS>
+__global__ void __launch_bounds__(256)
+k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base, uint32_t* __restrict__ next,
+              const unsigned long long* __restrict__ parents, unsigned long long next_base,
+              unsigned long long next_cap, DevCounters* ctr) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ unsigned int cov[COVER_CODES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int W = L.W, AW = L.all_words;
+  uint32_t* rows = lds + wave * lane_lds_words(W, AW);
+  uint32_t* prow = rows + lane * W;
+  const LaneWords pall{rows + 64 * W + lane};
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
+  __syncthreads();
+  const unsigned long long begin = ctr->mat_begin;
+  const unsigned long long end = min(ctr->next_count, next_cap);
+  for (unsigned long long g = begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; g < end;
+       g += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const unsigned long long slot = g + lane;
+    if (slot < end) {
+      const unsigned long long pr = parents[next_base + slot];
+      const unsigned long long sidx = ((pr >> 16) & ((1ull << 40) - 1ull)) - cur_base;
+      const int inst = (int)(pr & 0xffffull);
+      const uint32_t* src = cur + sidx * (unsigned long long)W;
+      for (int w = 0; w < W; w++) prow[w] = src[w];
+      const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
+      Delta d;
+      compute_delta<NS>(L, prow, inst, d);
+      const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
+      materialize<NS>(L, prow, d, pall, cfp, next + slot * (unsigned long long)W);
+      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+      if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+        ctr->viol_parent = sidx + cur_base;
+        ctr->viol_inst = inst;
+        ctr->viol_in_model = 1;
+        ctr->viol_child = next_base + slot;
+      }
+      atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
+    if (cov[k]) atomicAdd(&ctr->cover[COVER_CODES + k], (unsigned long long)cov[k]);
 }
 
 // Owner side of the exchange: insert the fingerprints other shards sent and
@@ -710,6 +793,11 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
   if (s_end <= s_begin) return hipSuccess;
   const int wpb = expand_lane_wpb(L);
   if (wpb > 0) {  // one lane per state (rows fit LDS)
+    {  // k_materialize's range starts at the next-frontier count before this launch
+      hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
+                                    hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return e;
+    }
     const uint64_t groups = (s_end - s_begin + 63) / 64;
     const uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
     const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
@@ -730,6 +818,14 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
       default: RTLA_LANE_CASE(5)
     }
 #undef RTLA_LANE_CASE
+    {
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    const int mgrid = 256 * 16;
+    RTLA_DISPATCH_N(L, k_materialize, dim3(mgrid), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)cur_base,
+                    next, (const unsigned long long*)parents, (unsigned long long)next_base,
+                    (unsigned long long)next_cap, ctr);
     return hipGetLastError();
   }
   // rows too wide for 64 per wave in LDS: one wave per state

@@ -226,6 +226,10 @@ RTLA_HD uint32_t m_f(uint64_t k, int lo, int bits) { return (uint32_t)(k >> lo) 
 struct FP {
   uint64_t a, b;
 };
+#ifdef RTLA_EXP_MIX1  // perf experiment only: one multiply per mix
+RTLA_HD uint64_t mix_a(uint64_t z) { z ^= z >> 32; z *= 0xbf58476d1ce4e5b9ull; return z ^ (z >> 29); }
+RTLA_HD uint64_t mix_b(uint64_t z) { z ^= z >> 31; z *= 0xff51afd7ed558ccdull; return z ^ (z >> 33); }
+#else
 RTLA_HD uint64_t mix_a(uint64_t z) {  // splitmix64 finalizer
   z ^= z >> 30; z *= 0xbf58476d1ce4e5b9ull;
   z ^= z >> 27; z *= 0x94d049bb133111ebull;
@@ -238,6 +242,7 @@ RTLA_HD uint64_t mix_b(uint64_t z) {  // murmur3 fmix64 (independent constants)
   z ^= z >> 33;
   return z;
 }
+#endif
 RTLA_HD FP fp_add(FP x, FP y) { return FP{x.a + y.a, x.b + y.b}; }
 RTLA_HD FP fp_sub(FP x, FP y) { return FP{x.a - y.a, x.b - y.b}; }
 RTLA_HD FP hash_u64(uint64_t tag, uint64_t x) {
@@ -408,6 +413,106 @@ RTLA_HD void without_message(const Layout& L, P row, Delta& d, uint64_t key) {
   }
 }
 
+// Fingerprint-only sink for compute_delta (the BFS probe pass).  The same
+// action code runs against it, but bag updates are folded straight into the
+// change of the message-multiset hash instead of being recorded as slot
+// writes: the fingerprint is order-free, so only (key, old count, new count)
+// matters.  Every action touches at most two distinct message keys, and the
+// two keys of Reply (raft.tla:129-130) always differ in type, so each op can
+// look its key up in the PARENT bag.
+struct DeltaFp {
+  int32_t enabled;
+  int32_t in_model;
+  int32_t sub;
+  int32_t err;
+  int32_t srv;
+  uint32_t rec[3 + NMAX];
+  int32_t nmsg;            // new number of bag slots in use
+  int32_t nmsg0;           // parent's
+  int32_t dcount;          // change of BagCardinality(messages)
+  int32_t elec;
+  uint32_t erec[2 + NMAX];
+  FP fmsg;                 // change of the message-multiset hash
+};
+
+template <class P>
+RTLA_HD int bag_find0(const Layout& L, P row, int n, uint64_t key, uint64_t* val) {
+  int hit = -1;
+  uint64_t v = 0;
+  for (int k = 0; k < n; k++) {
+    const uint64_t x = bag_slot(L, row, k);
+    if (hit < 0 && m_key(x) == key) { hit = k; v = x; }
+  }
+  *val = v;
+  return hit;
+}
+// count c -> c + dc of message `key` (c = 0: absent), for the probe pass
+RTLA_HD void fp_bag_count(const Layout& L, DeltaFp& d, uint64_t key, uint32_t c, int dc) {
+  const uint32_t n = (uint32_t)((int)c + dc);
+  if ((int)n > L.C) d.in_model = 0;
+  d.dcount += dc;
+  if (c) d.fmsg = fp_sub(d.fmsg, h_msg(key | (uint64_t)c << 60));
+  if (n) d.fmsg = fp_add(d.fmsg, h_msg(key | (uint64_t)n << 60));
+}
+template <class P>
+RTLA_HD void with_message(const Layout& L, P row, DeltaFp& d, uint64_t key) {  // raft.tla:106-110
+  uint64_t v;
+  if (bag_find0(L, row, d.nmsg0, key, &v) >= 0) {
+    fp_bag_count(L, d, key, m_count(v), 1);
+  } else {
+    if (d.nmsg >= L.K) { d.err = 2; return; }
+    d.nmsg++;
+    fp_bag_count(L, d, key, 0, 1);
+  }
+}
+template <class P>
+RTLA_HD void without_message(const Layout& L, P row, DeltaFp& d, uint64_t key) {  // raft.tla:114-119
+  uint64_t v;
+  if (bag_find0(L, row, d.nmsg0, key, &v) < 0) return;
+  if (m_count(v) <= 1) d.nmsg--;
+  fp_bag_count(L, d, key, m_count(v), -1);
+}
+template <class P>
+RTLA_HD void bag_dup_slot(const Layout& L, P row, DeltaFp& d, int x) {  // DuplicateMessage :443-445
+  const uint64_t v = bag_slot(L, row, x);
+  fp_bag_count(L, d, m_key(v), m_count(v), 1);
+}
+template <class P>
+RTLA_HD void bag_dup_slot(const Layout& L, P row, Delta& d, int x) {
+  bag_set(L, row, d, x, bag_slot(L, row, x) + (1ull << 60));
+}
+RTLA_HD void delta_reset(Delta& d) { d.nops = 0; }
+RTLA_HD void delta_reset(DeltaFp& d) {
+  d.nmsg0 = d.nmsg; d.dcount = 0; d.fmsg = FP{0, 0};
+}
+// message part of the state constraint (specs/MC.tla StateConstraint)
+template <class P>
+RTLA_HD void bag_constraint(const Layout& L, P row, Delta& d) {
+  if (!d.nops) return;
+  int total_delta = 0;
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    if (q < d.nops) {
+      if ((int)m_count(d.op_new[q]) > L.C) d.in_model = 0;
+      total_delta += (int)m_count(d.op_new[q]) - (int)m_count(d.op_old[q]);
+    }
+  }
+  if (L.M > 0 && total_delta > 0) {
+    int total = 0;
+    const int nm = row_nmsg(L, row);
+    for (int k = 0; k < nm; k++) total += (int)m_count(bag_slot(L, row, k));
+    if (total + total_delta > L.M) d.in_model = 0;
+  }
+}
+template <class P>
+RTLA_HD void bag_constraint(const Layout& L, P row, DeltaFp& d) {
+  if (L.M > 0 && d.dcount > 0) {
+    int total = 0;
+    for (int k = 0; k < d.nmsg0; k++) total += (int)m_count(bag_slot(L, row, k));
+    if (total + d.dcount > L.M) d.in_model = 0;
+  }
+}
+
 template <int NS, class P>
 RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
   const int SW = 3 + RTLA_NSRV(L);
@@ -418,12 +523,13 @@ RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
 
 // Compute the successor of `row` under action instance `inst` (0..L.fam[F_COUNT]).
 // Follows raft.tla:454-463; allLogs' (:465) is applied per parent by the caller.
-template <int NS, class P>
-RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
+template <int NS, class P, class D>
+RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
   const int N = RTLA_NSRV(L);
   const int SW = 3 + N;
-  d.enabled = 0; d.in_model = 1; d.sub = R_NONE; d.err = 0; d.srv = -1; d.nops = 0;
+  d.enabled = 0; d.in_model = 1; d.sub = R_NONE; d.err = 0; d.srv = -1;
   d.nmsg = row_nmsg(L, row); d.elec = 0;
+  delta_reset(d);
   int fam = 0;
 #pragma unroll
   for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
@@ -610,7 +716,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
     }
   } else if (fam == F_DUPLICATE) {              // DuplicateMessage(m) :443-445
     if (x >= d.nmsg) return;
-    bag_set(L, row, d, x, bag_slot(L, row, x) + (1ull << 60));
+    bag_dup_slot(L, row, d, x);
     d.enabled = 1;
   } else {                                      // DropMessage(m) :448-450
     if (x >= d.nmsg) return;
@@ -622,22 +728,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, Delta& d) {
   if (d.srv >= 0) {
     if ((int)s_term(d.rec[0]) > L.T || (int)log_len(d.rec[1]) > L.L) d.in_model = 0;
   }
-  if (d.nops) {
-    int total_delta = 0;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-      if (q < d.nops) {
-        if ((int)m_count(d.op_new[q]) > L.C) d.in_model = 0;
-        total_delta += (int)m_count(d.op_new[q]) - (int)m_count(d.op_old[q]);
-      }
-    }
-    if (L.M > 0 && total_delta > 0) {
-      int total = 0;
-      const int nm = row_nmsg(L, row);
-      for (int k = 0; k < nm; k++) total += (int)m_count(bag_slot(L, row, k));
-      if (total + total_delta > L.M) d.in_model = 0;
-    }
-  }
+  bag_constraint(L, row, d);
 }
 
 // Fingerprint change of the delta (allLogs change excluded: per parent).
@@ -660,6 +751,25 @@ RTLA_HD FP delta_fp(const Layout& L, P row, const Delta& d, const FP* h_old_srv 
 #pragma unroll
   for (int q = 0; q < 3; q++)
     if (q < d.nops) f = fp_add(f, fp_sub(h_msg(d.op_new[q]), h_msg(d.op_old[q])));
+  if (d.elec) f = fp_add(f, h_elec(d.erec, 2 + RTLA_NSRV(L)));
+  return f;
+}
+
+template <int NS, class P>
+RTLA_HD FP delta_fp(const Layout& L, P row, const DeltaFp& d, const FP* h_old_srv = nullptr) {
+  const int SW = 3 + RTLA_NSRV(L);
+  FP f = d.fmsg;
+  if (d.srv >= 0) {
+    FP old;
+    if (h_old_srv) {
+      old = *h_old_srv;
+    } else {
+      uint32_t orec[3 + NMAX];
+      load_rec<NS>(L, row, d.srv, orec);
+      old = h_srv(d.srv, orec, SW);
+    }
+    f = fp_add(f, fp_sub(h_srv(d.srv, d.rec, SW), old));
+  }
   if (d.elec) f = fp_add(f, h_elec(d.erec, 2 + RTLA_NSRV(L)));
   return f;
 }

@@ -20,7 +20,7 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtla.so")
+LIB_PATH = os.environ.get("RTLA_LIB") or os.path.join(HERE, "librtla.so")  # RTLA_LIB: perf-experiment builds only
 
 OK, DONE, VIOLATION = 0, 1, 2
 INV_BITS = {"NoTwoLeaders": 1, "ElectionSafety": 2, "LogMatching": 4}
