@@ -136,6 +136,13 @@ int rtla_row_fingerprint(const rtla_cfg *cfg, const uint32_t *row, uint64_t out[
 const char *rtla_strerror(int status);
 int rtla_abi_version(void);
 
+/* Diagnostic (performance analysis only): re-expand the current frontier
+ * `reps` times with k_expand_lane switches `xflags` (1 = no fingerprint-set
+ * probe, 2 = no coverage counters, 4 = trivial fingerprint delta, 8 = no
+ * k_materialize); *ms = mean device time per launch.  Pollutes the search
+ * state: use only after the last rtla_step. */
+int rtla_time_expand(rtla_ctx *ctx, int xflags, int reps, double *ms);
+
 /* Calibration: n random 8-byte CAS inserts into a table of 2^log2 slots;
  * returns device seconds. */
 int rtla_probe_bench(int log2, uint64_t n, double *seconds, uint64_t *inserted);

@@ -36,6 +36,14 @@ struct ShardBox {
   unsigned long long* send_ref;   // [nshard][cap]: local parent index << 16 | instance
 };
 
+// Diagnostic switches of k_expand_lane (rtla_time_expand only; 0 in the BFS).
+enum {
+  XF_NO_PROBE = 1,        // skip the fingerprint-set CAS (every successor "seen")
+  XF_NO_COVER = 2,        // skip the coverage counters
+  XF_NO_HASH = 4,         // replace the fingerprint delta by a trivial sum
+  XF_NO_MATERIALIZE = 8,  // do not launch k_materialize
+};
+
 // Per-level device counters (zeroed before each level except `cover`).
 struct DevCounters {
   unsigned long long generated;

@@ -892,6 +892,36 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
   return rc;
 }
 
+// Diagnostic: re-expand the current frontier `reps` times with the given
+// k_expand_lane switches (XF_*) and report the mean device time per launch.
+// Successors are inserted into the fingerprint set (so later reps find them
+// seen) and written to the idle frontier buffer: call it only at the end of
+// a search, never between rtla_step calls whose results matter.
+extern "C" int rtla_time_expand(rtla_ctx* x, int xflags, int reps, double* ms) {
+  if (!x || reps < 1 || !ms) return RTLA_E_ARG;
+  if (x->sh.size() != 1 || x->nshard != 1) return RTLA_E_STATE;
+  HIPCHK(hipSetDevice(x->device));
+  Shard& s = x->sh[0];
+  const uint64_t next_base = s.cur_base + s.n_cur;
+  if (next_base >= s.parents_cap) return RTLA_E_OVERFLOW;
+  const uint64_t next_cap = std::min<uint64_t>(x->front_cap, s.parents_cap - next_base);
+  ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+  float total = 0.f;
+  for (int r = 0; r < reps; r++) {
+    HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
+    HIPCHK(hipEventRecord(s.ev0, x->stream));
+    HIPCHK(launch_expand(x->L, s.front[s.cur], 0, s.n_cur, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base,
+                         next_cap, s.table, x->tlog2, s.ctr, box, x->grid, x->stream, xflags));
+    HIPCHK(hipEventRecord(s.ev1, x->stream));
+    HIPCHK(hipEventSynchronize(s.ev1));
+    float m = 0.f;
+    HIPCHK(hipEventElapsedTime(&m, s.ev0, s.ev1));
+    total += m;
+  }
+  *ms = total / reps;
+  return RTLA_OK;
+}
+
 extern "C" int rtla_probe_bench(int log2, uint64_t n, double* seconds, uint64_t* inserted) {
   uint64_t* table = nullptr;
   DevCounters* ctr = nullptr;

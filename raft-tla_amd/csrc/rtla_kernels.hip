@@ -82,7 +82,7 @@ __device__ __forceinline__ int candidate_inst(const Layout& L, int q, int nmsg) 
   if (q < fixed) return q;
   int r = q - fixed;
   int fam = r / nmsg, slot = r - fam * nmsg;
-  return L.fam[F_RECEIVE + fam] + slot;
+  return fam_base(L, F_RECEIVE + fam) + slot;
 }
 
 __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
@@ -307,7 +307,7 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
 __device__ __forceinline__ int wave_inst(const Layout& L, int q, int fixed, int kmax) {
   if (q < fixed) return q;
   const int r = q - fixed, fam = r / kmax;
-  return L.fam[F_RECEIVE + fam] + (r - fam * kmax);
+  return fam_base(L, F_RECEIVE + fam) + (r - fam * kmax);
 }
 
 template <int NS>
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_L
 k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
               unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
               unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
-              DevCounters* ctr, ShardBox box) {
+              DevCounters* ctr, ShardBox box, int xflags) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -390,11 +390,12 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
         bool probe = false;
         unsigned long long key = 0, idx = 0;
         if (en && d.in_model) {
-          const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
+          const FP cfp = (xflags & XF_NO_HASH) ? FP{pfp.a + d.rec[0] + (uint64_t)d.fmsg.a, pfp.b + d.rec[1]}
+                                                : fp_add(pfp, delta_fp<NS>(L, prow, d));
           if (cfp.a != pfp0.a || cfp.b != pfp0.b) {  // successor == parent: already in the set
             const int owner = MULTI ? fp_owner(cfp, G) : 0;
             if (!MULTI || owner == box.me) {
-              probe = true;
+              probe = !(xflags & XF_NO_PROBE);
               key = cfp.b | 1ull;
               idx = cfp.a >> (64 - tlog2);
             } else {
@@ -405,10 +406,8 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
           }
         }
         // generated coverage: the family is uniform; Receive's sub-action is per lane
-#ifdef RTLA_EXP_NOCOV
-        if (0)
-#endif
-        if (q < fixed || (q - fixed) / kmax != 0) {
+        if (xflags & XF_NO_COVER) {
+        } else if (q < fixed || (q - fixed) / kmax != 0) {
           const int c1 = __popcll(__ballot(en));
           if (lane == 0 && c1) atomicAdd(&cov[cover_code(L, inst, R_NONE)], (unsigned)c1);
         } else {
@@ -789,7 +788,7 @@ int expand_blocks_per_cu(const Layout& L) {
 
 hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
                          uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
-                         int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st) {
+                         int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags) {
   if (s_end <= s_begin) return hipSuccess;
   const int wpb = expand_lane_wpb(L);
   if (wpb > 0) {  // one lane per state (rows fit LDS)
@@ -808,7 +807,7 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)s_begin, \
                        (unsigned long long)s_end, (unsigned long long)cur_base, next, (unsigned long long*)parents, \
                        (unsigned long long)next_base, (unsigned long long)next_cap, (unsigned long long*)table,  \
-                       tlog2, ctr, box);                                                                      \
+                       tlog2, ctr, box, xflags);                                                              \
   } break;
     switch (L.N) {
       RTLA_LANE_CASE(1)
@@ -822,6 +821,7 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
+    if (xflags & XF_NO_MATERIALIZE) return hipSuccess;
     const int mgrid = 256 * 16;
     RTLA_DISPATCH_N(L, k_materialize, dim3(mgrid), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)cur_base,
                     next, (const unsigned long long*)parents, (unsigned long long)next_base,

@@ -18,7 +18,7 @@ int expand_blocks_per_cu(const Layout& L);
 hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end,
                          uint64_t cur_base, uint32_t* next, uint64_t* parents, uint64_t next_base,
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
-                         int grid, hipStream_t st);
+                         int grid, hipStream_t st, int xflags = 0);
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
                                 hipStream_t st);

@@ -132,6 +132,24 @@ static inline int make_layout(Layout* l, int N, int V, int T, int L, int C, int 
   return 0;
 }
 
+// Run-time-indexed reads of the Layout tables as select chains: on the GPU a
+// dynamically indexed kernel-argument array becomes a vector memory load, and
+// its vmcnt wait would also wait for every fingerprint-set CAS in flight.
+RTLA_HD int fam_base(const Layout& L, int fam) {
+  int r = 0;
+#pragma unroll
+  for (int f = 0; f <= F_COUNT; f++)
+    if (f == fam) r = L.fam[f];
+  return r;
+}
+RTLA_HD int log_off_at(const Layout& L, int n) {
+  int r = 0;
+#pragma unroll
+  for (int k = 0; k < LMAX + 2; k++)
+    if (k == n) r = L.log_off[k];
+  return r;
+}
+
 // ------------------------------------------------------------- fields ----
 RTLA_HD uint32_t s_term(uint32_t w) { return w & 15u; }
 RTLA_HD uint32_t s_role(uint32_t w) { return (w >> 4) & 3u; }
@@ -180,7 +198,7 @@ RTLA_HD int log_index(const Layout& L, uint32_t l) {
     idx += d * pw;
     pw *= B;
   }
-  return L.log_off[n] + idx;
+  return log_off_at(L, n) + idx;
 }
 RTLA_HD uint32_t log_from_index(const Layout& L, int idx) {
   int n = 0;
@@ -533,7 +551,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
   int fam = 0;
 #pragma unroll
   for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
-  const int x = inst - L.fam[fam];
+  const int x = inst - fam_base(L, fam);
   uint32_t* rec = d.rec;
 
   if (fam == F_RESTART) {                       // Restart(i) :167-175

@@ -71,6 +71,7 @@ def _load():
         "rtla_frontier": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_size_t)]),
         "rtla_coverage": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int]),
         "rtla_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+        "rtla_time_expand": (C.c_int, [C.c_void_p, C.c_int, C.c_int, P(C.c_double)]),
         "rtla_row_words": (C.c_int, [P(_Cfg)]),
         "rtla_init_row": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
         "rtla_expand_batch": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, P(C.c_uint32),
@@ -96,7 +97,7 @@ _lib = _load()
 EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset", "rtla_step", "rtla_violation",
             "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
-            "rtla_strerror", "rtla_abi_version", "rtla_probe_bench"]
+            "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand"]
 
 
 @dataclass(frozen=True)
@@ -334,6 +335,12 @@ class Checker:
         buf = (C.c_uint32 * max(1, n.value * w))()
         _check(_lib.rtla_frontier(self._h, buf, n.value, C.byref(n)), "rtla_frontier")
         return [list(buf[k * w:(k + 1) * w]) for k in range(n.value)]
+
+    def time_expand(self, xflags: int, reps: int = 3) -> float:
+        """Diagnostic: mean ms of re-expanding the current frontier (pollutes the search)."""
+        ms = C.c_double()
+        _check(_lib.rtla_time_expand(self._h, xflags, reps, C.byref(ms)), "rtla_time_expand")
+        return ms.value
 
     def coverage(self) -> dict:
         n = len(COVER_NAMES)
