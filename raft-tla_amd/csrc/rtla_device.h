@@ -42,6 +42,12 @@ enum {
   XF_NO_COVER = 2,        // skip the coverage counters
   XF_NO_HASH = 4,         // replace the fingerprint delta by a trivial sum
   XF_NO_MATERIALIZE = 8,  // do not launch k_materialize
+  XF_LANE_KERNEL = 16,    // use k_expand_lane (no compaction) for a single shard
+  XF_NO_CHUNKS = 32,      // compact kernel: load rows + per-state setup only
+  XF_NO_DELTA = 64,       // compact kernel: compaction without evaluating actions
+  XF_GENERIC_DELTA = 128, // compact kernel: never use the per-family specialised evaluation
+  XF_BLOCK1 = 256,        // compact kernel: 1-wave workgroups instead of 4
+  XF_NO_PERSIST = 512,    // compact kernel: one group per wave instead of persistent waves
 };
 
 // Per-level device counters (zeroed before each level except `cover`).

@@ -446,6 +446,17 @@ extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
   return RTLA_OK;
 }
 
+// RTLA_XFLAGS: kernel-variant switches (XF_* in rtla_device.h) for performance
+// experiments; results are identical for the variants that do not skip work.
+static int env_xflags() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTLA_XFLAGS");
+    v = e ? (atoi(e) & (XF_LANE_KERNEL | XF_GENERIC_DELTA | XF_BLOCK1 | XF_NO_PERSIST)) : 0;
+  }
+  return v;
+}
+
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -645,7 +656,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     uint64_t blocks = (s.n_cur + 3) / 4;
     int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
     HIPCHK(launch_expand(L, s.front[s.cur], 0, s.n_cur, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[0],
-                         next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream));
+                         next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags()));
   } else {
     // lock-step chunks over the frontier; every shard runs the same number
     uint64_t mx = 0;

@@ -85,6 +85,13 @@ __device__ __forceinline__ int candidate_inst(const Layout& L, int q, int nmsg) 
   return fam_base(L, F_RECEIVE + fam) + slot;
 }
 
+__device__ __forceinline__ int inst_family(const Layout& L, int inst) {
+  int fam = 0;
+#pragma unroll
+  for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
+  return fam;
+}
+
 __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
   int fam = 0;
 #pragma unroll
@@ -524,6 +531,281 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
+// ------------------------------------------------------------------------
+// k_expand_compact: the single-shard BFS level kernel with work compaction.
+//
+// Like k_expand_lane, a wave owns 64 frontier rows in LDS.  Each lane first
+// computes, for its own state, the bit mask of action instances whose
+// enabling guard holds (the guards of raft.tla's actions, below).  The wave
+// then lists the (state, instance) pairs in instance-major order -- so
+// consecutive pairs belong to the same family of Next -- and evaluates them
+// 64 at a time, one pair per lane.  Every lane of a chunk does useful work
+// and a chunk spans at most a few families, instead of sweeping all ~45
+// instances with most lanes idle.  Fingerprint-set CAS of chunk c are
+// resolved after chunk c+1 is computed; new states go to a per-wave LDS list
+// and reserve next-frontier slots 64+ at a time (one atomic per flush).
+namespace {
+
+constexpr int RING = 128;   // pair ring (u16: state lane << 8 | instance - window base)
+constexpr int NEWCAP = 128; // new-state list (u64 parent records)
+
+__host__ __device__ constexpr int compact_lds_words(int W, int AW) {
+  return 64 * W + 64 * AW + RING / 2 + 2 * NEWCAP;
+}
+
+// bits << off into a 64-bit window mask (off may be negative or >= 64)
+__device__ __forceinline__ unsigned long long win_bits(unsigned long long bits, int off) {
+  if (off >= 64 || off <= -64) return 0ull;
+  return off >= 0 ? bits << off : bits >> (-off);
+}
+
+// Instances [wb, wb+64) whose enabling guard holds in `row`.  A superset is
+// safe (compute_delta re-checks every guard); a subset would lose states.
+template <int NS>
+__device__ __forceinline__ unsigned long long cand_mask(const Layout& L, const uint32_t* row, int nmsg, int wb) {
+  constexpr int N = NS;
+  const int SW = 3 + N;
+  unsigned long long rv = 0, bl = 0, ldr = 0, tmo = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint32_t w0 = row[L.off_srv + i * SW];
+    const uint32_t role = s_role(w0);
+    if (role == FOLLOWER || role == CANDIDATE) tmo |= 1ull << i;          // Timeout :178-181
+    if (role == CANDIDATE) {
+      rv |= (unsigned long long)(~s_vresp(w0) & ((1u << N) - 1u)) << (i * N);  // RequestVote :190-192
+      if (__builtin_popcount(s_vgrant(w0)) * 2 > N) bl |= 1ull << i;     // BecomeLeader :229-231
+    }
+    if (role == LEADER) ldr |= 1ull << i;                                 // :204-206, :246-248, :259-260
+  }
+  unsigned long long ae = 0, cr = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    if (ldr >> i & 1ull) {
+      ae |= (((1ull << N) - 1ull) & ~(1ull << i)) << (i * N);             // AppendEntries i /= j
+      cr |= ((1ull << L.V) - 1ull) << (i * L.V);                           // ClientRequest(i, v)
+    }
+  const unsigned long long bag = nmsg >= 64 ? ~0ull : ((1ull << nmsg) - 1ull);
+  unsigned long long m = 0;
+  m |= win_bits((1ull << N) - 1ull, L.fam[F_RESTART] - wb);               // Restart: always
+  m |= win_bits(tmo, L.fam[F_TIMEOUT] - wb);
+  m |= win_bits(rv, L.fam[F_REQUESTVOTE] - wb);
+  m |= win_bits(bl, L.fam[F_BECOMELEADER] - wb);
+  m |= win_bits(cr, L.fam[F_CLIENTREQUEST] - wb);
+  m |= win_bits(ldr, L.fam[F_ADVANCECOMMIT] - wb);
+  m |= win_bits(ae, L.fam[F_APPENDENTRIES] - wb);
+  m |= win_bits(bag, L.fam[F_RECEIVE] - wb);
+  m |= win_bits(bag, L.fam[F_DUPLICATE] - wb);
+  m |= win_bits(bag, L.fam[F_DROP] - wb);
+  return m;
+}
+
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return (unsigned long long)lo | (unsigned long long)hi << 32;
+}
+
+}  // namespace
+
+#ifndef RTLA_COMPACT_WAVES_PER_EU
+#define RTLA_COMPACT_WAVES_PER_EU 1
+#endif
+template <int NS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_COMPACT_WAVES_PER_EU)))
+k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
+                 unsigned long long cur_base, unsigned long long* __restrict__ parents, unsigned long long next_base,
+                 unsigned long long next_cap, unsigned long long* table, int tlog2, DevCounters* ctr, int me,
+                 int xflags) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ unsigned int cov[2 * COVER_CODES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int W = L.W, AW = L.all_words;
+  uint32_t* rows = lds + wave * compact_lds_words(W, AW);
+  const LaneWords pall_mine{rows + 64 * W + lane};
+  uint16_t* ring = reinterpret_cast<uint16_t*>(rows + 64 * W + 64 * AW);
+  unsigned long long* newl = reinterpret_cast<unsigned long long*>(rows + 64 * W + 64 * AW + RING / 2);
+  for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
+  __syncthreads();
+
+  unsigned my_gen = 0, my_probe = 0;
+  const int ninst = L.fam[F_COUNT];
+  const unsigned long long lanes_below = (1ull << lane) - 1ull;
+  // pending probe (issued by the previous chunk)
+  bool pend = false;
+  unsigned long long pold = 0, pkey = 0, pidx = 0, prec = 0;
+  int nnew = 0;  // entries in newl (uniform)
+
+  auto flush_new = [&]() {
+    // reserve nnew slots with one atomic, then write the parent records
+    unsigned long long obase = 0;
+    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)nnew);
+    obase = shfl0_u64(obase);
+    if (obase + nnew > next_cap) {
+      if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    } else {
+      for (int k = lane; k < nnew; k += 64) parents[next_base + obase + k] = newl[k];
+    }
+    wave_sync();
+    nnew = 0;
+  };
+  auto resolve = [&]() {
+    bool isnew = false;
+    if (pend) isnew = fpset_resolve(table, tlog2, pkey, pidx, pold, ctr);
+    const unsigned long long m = __ballot(isnew);
+    if (m) {
+      if (isnew) newl[nnew + __popcll(m & lanes_below)] = prec;
+      nnew += __popcll(m);
+      wave_sync();
+      if (nnew >= 64) flush_new();
+    }
+    pend = false;
+  };
+
+  for (unsigned long long s0 = s_begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; s0 < s_end;
+       s0 += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const int nvalid = (int)min<unsigned long long>(64ull, s_end - s0);
+    {
+      const uint32_t* src = cur + s0 * (unsigned long long)W;
+      const int nw = nvalid * W;
+      for (int w = lane; w < nw; w += 64) rows[w] = src[w];
+    }
+    wave_sync();
+    const bool valid = lane < nvalid;
+    const uint32_t* prow_mine = rows + lane * W;
+    FP pfp0{0, 0}, pfp{0, 0};
+    int nmsg = 0;
+    if (valid) {
+      pfp0 = row_fp(prow_mine);
+      pfp = fp_add(pfp0, alllogs_delta<NS>(L, prow_mine, pall_mine));
+      nmsg = row_nmsg(L, prow_mine);
+    }
+    for (int wb = 0; wb < ((xflags & XF_NO_CHUNKS) ? 0 : ninst); wb += 64) {
+      const unsigned long long mask = valid ? cand_mask<NS>(L, prow_mine, nmsg, wb) : 0ull;
+      unsigned long long todo = wave_or_u64(mask);
+      int pos = 0, done = 0, cfam = -1;
+      while (todo || pos > done) {
+        // Append the pairs of the next instance(s) until a chunk is ready.  A
+        // chunk is cut at a family boundary once it is a third full, so most
+        // chunks hold one family and take the specialised path below.
+        while (todo && pos - done < 64) {
+          const int q = __builtin_ctzll(todo);
+          const int f = inst_family(L, wb + q);
+          if (f != cfam && pos - done >= 22) break;
+          cfam = f;
+          todo &= todo - 1;
+          const bool mine = (mask >> q) & 1ull;
+          if (f == F_RECEIVE) {  // group by message type: one handler of raft.tla:421-436 per run
+            const uint32_t ty = mine ? m_type(bag_slot(L, prow_mine, wb + q - L.fam[F_RECEIVE])) : 0u;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; t++) {
+              const bool b = mine && ty == t;
+              const unsigned long long m = __ballot(b);
+              if (b) ring[(pos + __popcll(m & lanes_below)) & (RING - 1)] = (uint16_t)(lane << 8 | q);
+              pos += __popcll(m);
+            }
+          } else {
+            const unsigned long long m = __ballot(mine);
+            if (mine) ring[(pos + __popcll(m & lanes_below)) & (RING - 1)] = (uint16_t)(lane << 8 | q);
+            pos += __popcll(m);
+          }
+        }
+        cfam = -1;
+        const int cnt = min(64, pos - done);
+        wave_sync();
+        // ---- one chunk: lane t evaluates pair done + t
+        const bool active = lane < cnt;
+        const int e = active ? ring[(done + lane) & (RING - 1)] : 0;
+        const int sl = e >> 8, inst = wb + (e & 255);
+        const uint32_t* prow = rows + sl * W;
+        const FP qfp{shfl_u64(pfp.a, sl), shfl_u64(pfp.b, sl)};
+        const FP qfp0{shfl_u64(pfp0.a, sl), shfl_u64(pfp0.b, sl)};
+        DeltaFp d;
+        d.enabled = 0;
+        if (!(xflags & XF_NO_DELTA)) {
+          const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
+          const int f1 = inst_family(L, __builtin_amdgcn_readlane(inst, cnt - 1));
+          if (f0 != f1 || (xflags & XF_GENERIC_DELTA)) {
+            if (active) compute_delta<NS>(L, prow, inst, d);
+          } else if (active) {
+            switch (f0) {  // one family in the whole chunk: its code only
+              case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
+              case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
+              case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
+              case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
+              case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
+              case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
+              case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
+              case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
+              case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
+              default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
+            }
+          }
+        }
+        bool en = d.enabled != 0;
+        if (en && d.err) {
+          set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
+          en = false;
+        }
+        my_gen += en ? 1u : 0u;
+        bool probe = false;
+        unsigned long long key = 0, idx = 0;
+        if (en && d.in_model) {
+          const FP cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
+                                                : fp_add(qfp, delta_fp<NS>(L, prow, d));
+          if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
+            probe = !(xflags & XF_NO_PROBE);
+            key = cfp.b | 1ull;
+            idx = cfp.a >> (64 - tlog2);
+          }
+        }
+        if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
+          const int code = en ? cover_code(L, inst, d.sub) : -1;
+          const unsigned long long em = __ballot(en);
+          if (em) {
+            const int c0 = __shfl(code, __builtin_ctzll(em));
+            const bool same = en && code == c0;
+            const int n0 = __popcll(__ballot(same));
+            if (lane == 0) atomicAdd(&cov[c0], (unsigned)n0);
+            if (en && !same) atomicAdd(&cov[code], 1u);
+          }
+        }
+        if (en && !d.in_model) {  // out-of-model successors: checked, never stored
+          const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+          if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+            ctr->viol_parent = cur_base + s0 + sl;
+            ctr->viol_inst = inst;
+            ctr->viol_in_model = 0;
+            ctr->viol_child = ~0ull;
+          }
+        }
+        resolve();  // the previous chunk's CAS, after this chunk's arithmetic
+        if (probe) {
+          my_probe++;
+          pend = true;
+          pkey = key;
+          pidx = idx;
+          prec = (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
+          pold = atomicCAS(&table[idx], 0ull, key);
+        }
+        done += cnt;
+      }
+    }
+    wave_sync();  // the next group overwrites this group's rows
+  }
+  resolve();
+  if (nnew) flush_new();
+  for (int off = 32; off > 0; off >>= 1) {
+    my_gen += __shfl_down(my_gen, off);
+    my_probe += __shfl_down(my_probe, off);
+  }
+  if (lane == 0 && my_gen) atomicAdd(&ctr->generated, (unsigned long long)my_gen);
+  if (lane == 0 && my_probe) atomicAdd(&ctr->probes, (unsigned long long)my_probe);
+  __syncthreads();
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
+    if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
+}
+
 // k_materialize: build the rows of the new states k_expand_lane found.
 // Slots [ctr->mat_begin, ctr->next_count) of the next frontier hold only a
 // parent record (shard << 56 | parent index << 16 | action instance); one
@@ -771,6 +1053,23 @@ int expand_lane_wpb(const Layout& L) {
   return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
 }
 
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+int expand_compact_wpb(const Layout& L) {
+  const size_t per = (size_t)compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+  if (per > 64 * 1024 || ((L.fam[F_COUNT] + 63) / 64) * 64 > 256) return 0;  // instance ids fit 8 bits per window
+  return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
+}
+
 int expand_blocks_per_cu(const Layout& L) {
   size_t per = expand_lds_bytes(L, 4) + 2 * COVER_CODES * sizeof(unsigned int);
   int b = (int)((160u * 1024u) / per);
@@ -790,6 +1089,34 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
                          uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
                          int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags) {
   if (s_end <= s_begin) return hipSuccess;
+  const int cwpb = expand_compact_wpb(L);
+  if (box.nshard == 1 && cwpb > 0 && !(xflags & XF_LANE_KERNEL)) {
+    {  // k_materialize's range starts at the next-frontier count before this launch
+      hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
+                                    hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return e;
+    }
+    const int wpb = (xflags & XF_BLOCK1) ? 1 : cwpb;
+    const uint64_t groups = (s_end - s_begin + 63) / 64;
+    uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
+    if (!(xflags & XF_NO_PERSIST))  // persistent waves: ~16 per CU, each loops over groups
+      blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * 16 / wpb);
+    const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+    RTLA_DISPATCH_N(L, k_expand_compact, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur,
+                    (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base,
+                    (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,
+                    (unsigned long long*)table, tlog2, ctr, box.me, xflags);
+    {
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    if (xflags & XF_NO_MATERIALIZE) return hipSuccess;
+    const size_t mlds = (size_t)cwpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+    RTLA_DISPATCH_N(L, k_materialize, dim3(256 * 16), dim3(64 * cwpb), mlds, st, L, cur, (unsigned long long)cur_base,
+                    next, (const unsigned long long*)parents, (unsigned long long)next_base,
+                    (unsigned long long)next_cap, ctr);
+    return hipGetLastError();
+  }
   const int wpb = expand_lane_wpb(L);
   if (wpb > 0) {  // one lane per state (rows fit LDS)
     {  // k_materialize's range starts at the next-frontier count before this launch

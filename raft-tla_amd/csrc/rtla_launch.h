@@ -12,6 +12,8 @@ size_t expand_lds_bytes(const Layout& L, int wpb);
 // Waves per block of the lane-per-state k_expand_lane (0: rows too wide,
 // the wave-per-state k_expand is used).
 int expand_lane_wpb(const Layout& L);
+// Waves per block of the compacting single-shard kernel (0: not usable).
+int expand_compact_wpb(const Layout& L);
 // Blocks of 4 waves that fit on one CU given the LDS footprint.
 int expand_blocks_per_cu(const Layout& L);
 

@@ -541,17 +541,22 @@ RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
 
 // Compute the successor of `row` under action instance `inst` (0..L.fam[F_COUNT]).
 // Follows raft.tla:454-463; allLogs' (:465) is applied per parent by the caller.
-template <int NS, class P, class D>
+// FAM >= 0: the caller guarantees inst belongs to that family (GPU chunks of
+// one family); the dispatch below then folds away at compile time.
+template <int NS, int FAM = -1, class P, class D>
 RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
   const int N = RTLA_NSRV(L);
   const int SW = 3 + N;
   d.enabled = 0; d.in_model = 1; d.sub = R_NONE; d.err = 0; d.srv = -1;
   d.nmsg = row_nmsg(L, row); d.elec = 0;
   delta_reset(d);
-  int fam = 0;
+  int fam = FAM;
+  if (FAM < 0) {
+    fam = 0;
 #pragma unroll
-  for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
-  const int x = inst - fam_base(L, fam);
+    for (int f = 1; f < F_COUNT; f++) fam += inst >= L.fam[f];
+  }
+  const int x = inst - (FAM >= 0 ? L.fam[FAM >= 0 ? FAM : 0] : fam_base(L, fam));
   uint32_t* rec = d.rec;
 
   if (fam == F_RESTART) {                       // Restart(i) :167-175

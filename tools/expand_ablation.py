@@ -17,8 +17,9 @@ with rtla.Checker(cfg) as ck:
         ck.step()
     lv = ck.levels[-1]
     print("frontier", lv.new, flush=True)
-    variants = [("full", 0), ("no_materialize", 8), ("no_cover", 2 | 8), ("no_hash", 4 | 8), ("no_probe", 1 | 8),
-                ("no_probe_no_hash_no_cover", 1 | 2 | 4 | 8), ("full_again", 0)]
+    variants = [("full", 0), ("no_materialize", 8), ("block4_nopersist", 256 | 512 | 8),
+                ("block1_nopersist", 512 | 8), ("block4_persist", 256 | 8), ("generic", 128 | 8),
+                ("noprobe_nocover", 1 | 2 | 8), ("compaction_only", 64 | 8 | 2)]
     for name, xf in variants:
         ms = ck.time_expand(xf, a.reps)
         print(json.dumps({"variant": name, "xflags": xf, "ms": ms, "states_per_s": lv.new / ms * 1e3}), flush=True)
