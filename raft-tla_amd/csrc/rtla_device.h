@@ -46,7 +46,7 @@ enum {
   XF_NO_CHUNKS = 32,      // compact kernel: load rows + per-state setup only
   XF_NO_DELTA = 64,       // compact kernel: compaction without evaluating actions
   XF_GENERIC_DELTA = 128, // compact kernel: never use the per-family specialised evaluation
-  XF_BLOCK1 = 256,        // compact kernel: 1-wave workgroups instead of 4
+  XF_BLOCK4 = 256,        // compact kernel: 4-wave workgroups instead of 1
   XF_NO_PERSIST = 512,    // compact kernel: one group per wave instead of persistent waves
 };
 

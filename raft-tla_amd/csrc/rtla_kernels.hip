@@ -831,18 +831,24 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
   const unsigned long long end = min(ctr->next_count, next_cap);
   for (unsigned long long g = begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; g < end;
        g += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const int nv = (int)min<unsigned long long>(64ull, end - g);
     const unsigned long long slot = g + lane;
-    if (slot < end) {
-      const unsigned long long pr = parents[next_base + slot];
-      const unsigned long long sidx = ((pr >> 16) & ((1ull << 40) - 1ull)) - cur_base;
-      const int inst = (int)(pr & 0xffffull);
-      const uint32_t* src = cur + sidx * (unsigned long long)W;
-      for (int w = 0; w < W; w++) prow[w] = src[w];
+    const bool act = lane < nv;
+    const unsigned long long pr = act ? parents[next_base + slot] : 0ull;
+    const unsigned long long sidx = ((pr >> 16) & ((1ull << 40) - 1ull)) - cur_base;
+    const int inst = (int)(pr & 0xffffull);
+    // gather the parent rows: one coalesced row read per slot (rows stay in L2)
+    for (int r = 0; r < nv; r++) {
+      const unsigned long long sr = readlane_u64(sidx, r);
+      const uint32_t* src = cur + sr * (unsigned long long)W;
+      for (int w = lane; w < W; w += 64) rows[r * W + w] = src[w];
+    }
+    wave_sync();
+    if (act) {
       const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
       Delta d;
       compute_delta<NS>(L, prow, inst, d);
       const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
-      materialize<NS>(L, prow, d, pall, cfp, next + slot * (unsigned long long)W);
       const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
       if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
         ctr->viol_parent = sidx + cur_base;
@@ -851,7 +857,15 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
         ctr->viol_child = next_base + slot;
       }
       atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
+      materialize<NS>(L, prow, d, pall, cfp, prow);  // in place: the parent row is not read again
     }
+    wave_sync();
+    {  // the group's rows are contiguous in the next frontier: coalesced stores
+      uint32_t* dst = next + g * (unsigned long long)W;
+      const int nw = nv * W;
+      for (int w = lane; w < nw; w += 64) dst[w] = rows[w];
+    }
+    wave_sync();
   }
   __syncthreads();
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
@@ -1096,11 +1110,26 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
                                     hipMemcpyDeviceToDevice, st);
       if (e != hipSuccess) return e;
     }
-    const int wpb = (xflags & XF_BLOCK1) ? 1 : cwpb;
+    const int wpb = (xflags & XF_BLOCK4) ? cwpb : 1;  // one-wave workgroups by default
     const uint64_t groups = (s_end - s_begin + 63) / 64;
     uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
-    if (!(xflags & XF_NO_PERSIST))  // persistent waves: ~16 per CU, each loops over groups
-      blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * 16 / wpb);
+    if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
+      static int per_cu[2][NMAX + 1];
+      int& pc = per_cu[wpb == 1][L.N];
+      if (!pc) {
+        const size_t l = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+        hipError_t e = hipErrorInvalidValue;
+        switch (L.N) {
+          case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<1>, 64 * wpb, l); break;
+          case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<2>, 64 * wpb, l); break;
+          case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<3>, 64 * wpb, l); break;
+          case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<4>, 64 * wpb, l); break;
+          default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<5>, 64 * wpb, l); break;
+        }
+        if (e != hipSuccess || pc < 1) pc = 16 / wpb;
+      }
+      blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * pc);
+    }
     const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
     RTLA_DISPATCH_N(L, k_expand_compact, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur,
                     (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base,
