@@ -71,6 +71,9 @@ def main():
                     help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 2^30 x 8 B = 8 GiB "
                          "holds the bench model at 14%% load. 0 = auto (40%% of free HBM)")
     ap.add_argument("--levels", action="store_true", help="print the per-level table to stderr")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
+                         "(the multi-GPU exchange protocol with device copies as transport)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -87,7 +90,8 @@ def main():
 
     shape = WORKLOADS[args.workload]
     n, v, t, l, c, m, inv = shape
-    cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=args.fpset_log2)
+    cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=args.fpset_log2, shards=args.shards,
+                      mem_budget=(200 << 30) if args.shards > 1 else 0)
     ck = rtla.Checker(cfg, rank=rank, world=world, comm_id=comm_id)
 
     def barrier():

@@ -76,9 +76,11 @@ struct Shard {
   uint64_t* new_count = nullptr;   // [G] device: new fingerprints we own, per source
   uint64_t* all_new = nullptr;     // [G][G] device (RCCL all-gather target)
   uint64_t* rows_in = nullptr;     // [G] device: rows received per source (this sub-round)
+  uint64_t* rows_base = nullptr;   // [G] device: next-frontier slot of each source's first row
   uint32_t* send_rows = nullptr;   // [G][rows_cap][W + 2]
   uint32_t* recv_rows = nullptr;   // [G][rows_cap][W + 2]
-  std::vector<uint64_t> h_out, h_in, h_new_out, h_new_in;
+  uint64_t* sent = nullptr;        // [2^tlog2] fingerprints this shard already sent to their owners
+  std::vector<uint64_t> h_out, h_in, h_new_out, h_new_in, h_all;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // violation found on this shard
   int viol_mask = 0, viol_in_model = 0, viol_inst = -1;
@@ -102,6 +104,7 @@ struct rtla_ctx {
   int level = 0;
   bool inited = false, finished = false;
   uint64_t distinct = 0, generated = 0;
+  uint64_t max_front = 0;  // largest frontier of any shard in the job (multi-shard round count)
   int grid = 0;
   std::vector<uint32_t> init_row;
 };
@@ -294,9 +297,9 @@ extern "C" int rtla_comm_id(void* out128) {
 }
 
 static void free_shard(Shard& s) {
-  void* ptrs[] = {s.table,    s.parents,  s.front[0], s.front[1], s.ctr,       s.dflags,    s.out_count,
+  void* ptrs[] = {s.table,    s.sent,     s.parents,  s.front[0], s.front[1], s.ctr,       s.dflags,    s.out_count,
                   s.in_count, s.all_count, s.send_fp, s.send_ref, s.send_ans,  s.recv_fp,   s.recv_ans,
-                  s.new_count, s.all_new, s.rows_in,  s.send_rows, s.recv_rows};
+                  s.new_count, s.all_new, s.rows_in,  s.rows_base, s.send_rows, s.recv_rows};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -325,7 +328,7 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
                               2ull * G * x->rows_cap * (L.W + 2) * 4
                         : 0;
   if (!x->front_cap) {
-    uint64_t used = tbytes + pbytes + boxb;
+    uint64_t used = tbytes * (G > 1 ? 2 : 1) + pbytes + boxb;
     uint64_t rest = budget > used ? budget - used : 0;
     x->front_cap = std::max<uint64_t>(rest / (2 * rowb), 1024);
   }
@@ -347,12 +350,16 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
     HIPCHK(hipMalloc(&s.new_count, 8 * G));
     HIPCHK(hipMalloc(&s.all_new, 8 * G * G));
     HIPCHK(hipMalloc(&s.rows_in, 8 * G));
+    HIPCHK(hipMalloc(&s.rows_base, 8 * G));
     HIPCHK(hipMalloc(&s.send_rows, 4ull * G * x->rows_cap * (L.W + 2)));
     HIPCHK(hipMalloc(&s.recv_rows, 4ull * G * x->rows_cap * (L.W + 2)));
     s.h_out.assign(G, 0);
     s.h_in.assign(G, 0);
     s.h_new_out.assign(G, 0);
     s.h_new_in.assign(G, 0);
+    s.h_all.assign((size_t)G * G, 0);
+    HIPCHK(hipMalloc(&s.sent, tbytes));
+    HIPCHK(hipMemsetAsync(s.sent, 0, tbytes, x->stream));
   }
   HIPCHK(hipMemsetAsync(s.table, 0, tbytes, x->stream));
   HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
@@ -398,7 +405,7 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
     x->chunk = cfg->chunk;
     if (!x->chunk) {
       x->chunk = (per / 8) / ((uint64_t)G * nmax * 48);
-      x->chunk = std::min<uint64_t>(std::max<uint64_t>(x->chunk, 1024), 1u << 20);
+      x->chunk = std::min<uint64_t>(std::max<uint64_t>(x->chunk, 1024), 4u << 20);
     }
     x->box_cap = x->chunk * nmax;
     // row regions: ~1/10 of the budget; winners beyond it ship in sub-rounds
@@ -408,7 +415,9 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   int tl = cfg->fpset_log2;
   if (!tl) {
     tl = 20;
-    while (tl < 34 && (8ull << (tl + 1)) <= per * 2 / 5) tl++;
+    // the fingerprint set (and, multi-shard, the equally sized sent cache): ~40% of the budget
+    const uint64_t tshare = G > 1 ? per / 5 : per * 2 / 5;
+    while (tl < 34 && (8ull << (tl + 1)) <= tshare) tl++;
   }
   if (tl < 10 || tl > 40) { rtla_close(x); return RTLA_E_CONFIG; }
   x->tlog2 = tl;
@@ -461,6 +470,21 @@ static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Sum of n1 u64 and max of n2 u64 over all ranks (one synchronisation); host in/out.
+static int allreduce2_u64(rtla_ctx* x, uint64_t* sum, int n1, uint64_t* mx, int n2) {
+  if (x->world == 1) return RTLA_OK;
+  HIPCHK(hipMemcpyAsync(x->red, sum, 8 * n1, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipMemcpyAsync(x->red + 32, mx, 8 * n2, hipMemcpyHostToDevice, x->stream));
+  NCCLCHK(ncclGroupStart());
+  NCCLCHK(ncclAllReduce(x->red, x->red, n1, ncclUint64, ncclSum, x->comm, x->stream));
+  NCCLCHK(ncclAllReduce(x->red + 32, x->red + 32, n2, ncclUint64, ncclMax, x->comm, x->stream));
+  NCCLCHK(ncclGroupEnd());
+  HIPCHK(hipMemcpyAsync(sum, x->red, 8 * n1, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipMemcpyAsync(mx, x->red + 32, 8 * n2, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return RTLA_OK;
+}
+
 // Sum (op 0) or max (op 1) of n u64 over all ranks; host in/out.
 static int allreduce_u64(rtla_ctx* x, uint64_t* v, int n, int op) {
   if (x->world == 1) return RTLA_OK;
@@ -476,12 +500,13 @@ extern "C" int rtla_reset(rtla_ctx* x) {
   HIPCHK(hipSetDevice(x->device));
   for (auto& s : x->sh) {
     HIPCHK(hipMemsetAsync(s.table, 0, 8ull << x->tlog2, x->stream));
+    if (s.sent) HIPCHK(hipMemsetAsync(s.sent, 0, 8ull << x->tlog2, x->stream));
     HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
     s.n_cur = 0; s.cur_base = 0; s.cur = 0;
     s.viol_mask = 0; s.viol_in_model = 0; s.viol_inst = -1; s.viol_parent = 0; s.viol_child = ~0ull;
   }
   HIPCHK(hipStreamSynchronize(x->stream));
-  x->inited = false; x->finished = false; x->level = 0; x->distinct = 0; x->generated = 0;
+  x->inited = false; x->finished = false; x->level = 0; x->distinct = 0; x->generated = 0; x->max_front = 0;
   return RTLA_OK;
 }
 
@@ -505,7 +530,7 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
     s.n_cur = 1;
   }
   HIPCHK(hipStreamSynchronize(x->stream));
-  x->level = 1; x->distinct = 1; x->generated = 1; x->inited = true;
+  x->level = 1; x->distinct = 1; x->generated = 1; x->inited = true; x->max_front = 1;
   int bad = check_invariants<0>(L, x->init_row.data(), (const Delta*)nullptr);
   int status = RTLA_OK;
   if (bad) {
@@ -524,52 +549,79 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
 }
 
 // ---- multi-shard exchange (transport: device copies for local shards, RCCL across ranks)
+//
+// One exchange round costs two host synchronisations: (1) after the expand
+// launches, to learn every (sender, owner) record count, which sizes the
+// fingerprint and answer transfers; (2) after the owners' inserts, to learn
+// every (owner, sender) winner count, which sizes the row transfers.
 
-// After expand: every shard knows h_out[p] (records queued for shard p).
-// Fill h_in[p] (records shard p sent here) and move the fingerprints.
-static int exchange_fps(rtla_ctx* x) {
+// (1) h_out[p] = records this shard queued for owner p, h_in[p] = records
+// owner-shard receives from p; in_count on the device.
+static int gather_counts(rtla_ctx* x) {
+  const int G = x->nshard;
+  if (x->world == 1) {
+    for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.h_out.data(), s.out_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+    for (auto& dst : x->sh)
+      for (auto& src : x->sh) dst.h_in[src.id] = src.h_out[dst.id];
+  } else {
+    Shard& s = x->sh[0];
+    NCCLCHK(ncclAllGather(s.out_count, s.all_count, G, ncclUint64, x->comm, x->stream));
+    HIPCHK(hipMemcpyAsync(s.h_all.data(), s.all_count, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+    for (int p = 0; p < G; p++) {
+      s.h_out[p] = s.h_all[(size_t)s.id * G + p];
+      s.h_in[p] = s.h_all[(size_t)p * G + s.id];
+    }
+  }
+  for (auto& s : x->sh)
+    for (int p = 0; p < G; p++)
+      if (s.h_out[p] > x->box_cap || s.h_in[p] > x->box_cap) {
+        report_flags(FLAG_OUTBOX_FULL);
+        x->finished = true;
+        return RTLA_E_OVERFLOW;
+      }
+  // h_in stays untouched until the next round's synchronisation
+  for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.in_count, s.h_in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
+  return RTLA_OK;
+}
+
+// Move the queued (fingerprint) records to their owners.
+static int move_fps(rtla_ctx* x) {
   const int G = x->nshard;
   const uint64_t cap = x->box_cap;
   if (x->world == 1) {
     for (auto& dst : x->sh)
       for (auto& src : x->sh) {
-        uint64_t n = src.h_out[dst.id];
-        dst.h_in[src.id] = n;
+        const uint64_t n = src.h_out[dst.id];
         if (n)
           HIPCHK(hipMemcpyAsync(dst.recv_fp + 2 * (uint64_t)src.id * cap, src.send_fp + 2 * (uint64_t)dst.id * cap,
                                 16 * n, hipMemcpyDeviceToDevice, x->stream));
       }
-    for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.in_count, s.h_in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
     return RTLA_OK;
   }
   Shard& s = x->sh[0];
-  NCCLCHK(ncclAllGather(s.out_count, s.all_count, G, ncclUint64, x->comm, x->stream));
-  std::vector<uint64_t> all((size_t)G * G);
-  HIPCHK(hipMemcpyAsync(all.data(), s.all_count, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
-  for (int p = 0; p < G; p++) s.h_in[p] = all[(size_t)p * G + s.id];
-  HIPCHK(hipMemcpyAsync(s.in_count, s.h_in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
   NCCLCHK(ncclGroupStart());
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
-    NCCLCHK(ncclSend(s.send_fp + 2 * (uint64_t)p * cap, 2 * s.h_out[p], ncclUint64, p, x->comm, x->stream));
-    NCCLCHK(ncclRecv(s.recv_fp + 2 * (uint64_t)p * cap, 2 * s.h_in[p], ncclUint64, p, x->comm, x->stream));
+    if (s.h_out[p]) NCCLCHK(ncclSend(s.send_fp + 2 * (uint64_t)p * cap, 2 * s.h_out[p], ncclUint64, p, x->comm, x->stream));
+    if (s.h_in[p]) NCCLCHK(ncclRecv(s.recv_fp + 2 * (uint64_t)p * cap, 2 * s.h_in[p], ncclUint64, p, x->comm, x->stream));
   }
   NCCLCHK(ncclGroupEnd());
   return RTLA_OK;
 }
 
-// Owners answered in recv_ans (0 = seen, 1 + rank = new); route the answers
-// back into send_ans and tell every sender how many winners each owner has
-// from it (h_new_out) and every owner how many rows to expect (h_new_in).
-static int exchange_answers(rtla_ctx* x) {
+// (2) Owners answered in recv_ans (0 = seen, 1 + rank = new): route the
+// answers back into send_ans; h_new_out[p] = winners owner p has from this
+// shard, h_new_in[p] = rows this owner will receive from p.
+static int move_answers(rtla_ctx* x) {
   const int G = x->nshard;
   const uint64_t cap = x->box_cap;
   if (x->world == 1) {
     for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.new_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
     for (auto& src : x->sh)
       for (auto& dst : x->sh) {
-        uint64_t n = src.h_out[dst.id];
+        const uint64_t n = src.h_out[dst.id];
         if (n)
           HIPCHK(hipMemcpyAsync(src.send_ans + (uint64_t)dst.id * cap, dst.recv_ans + (uint64_t)src.id * cap, 4 * n,
                                 hipMemcpyDeviceToDevice, x->stream));
@@ -583,54 +635,59 @@ static int exchange_answers(rtla_ctx* x) {
   NCCLCHK(ncclGroupStart());
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
-    NCCLCHK(ncclSend(s.recv_ans + (uint64_t)p * cap, s.h_in[p], ncclUint32, p, x->comm, x->stream));
-    NCCLCHK(ncclRecv(s.send_ans + (uint64_t)p * cap, s.h_out[p], ncclUint32, p, x->comm, x->stream));
+    if (s.h_in[p]) NCCLCHK(ncclSend(s.recv_ans + (uint64_t)p * cap, s.h_in[p], ncclUint32, p, x->comm, x->stream));
+    if (s.h_out[p]) NCCLCHK(ncclRecv(s.send_ans + (uint64_t)p * cap, s.h_out[p], ncclUint32, p, x->comm, x->stream));
   }
   NCCLCHK(ncclGroupEnd());
   NCCLCHK(ncclAllGather(s.new_count, s.all_new, G, ncclUint64, x->comm, x->stream));
-  std::vector<uint64_t> all((size_t)G * G);
-  HIPCHK(hipMemcpyAsync(all.data(), s.all_new, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipMemcpyAsync(s.h_all.data(), s.all_new, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   for (int p = 0; p < G; p++) {
-    s.h_new_in[p] = all[(size_t)s.id * G + p];   // owner s.id: new from source p
-    s.h_new_out[p] = all[(size_t)p * G + s.id];  // owner p: new from us
+    s.h_new_in[p] = s.h_all[(size_t)s.id * G + p];   // owner s.id: new from source p
+    s.h_new_out[p] = s.h_all[(size_t)p * G + s.id];  // owner p: new from us
   }
   return RTLA_OK;
 }
 
-// Ship the winners of ranks [lo, lo + rows_cap) to their owners.
-static int exchange_rows(rtla_ctx* x, uint64_t lo) {
+// Largest winner count of any (owner, sender) pair in the whole job: every
+// rank runs the same number of row sub-rounds.
+static uint64_t most_winners(rtla_ctx* x) {
+  uint64_t most = 0;
+  if (x->world == 1) {
+    for (auto& s : x->sh)
+      for (uint64_t v : s.h_new_in) most = std::max(most, v);
+  } else {
+    for (uint64_t v : x->sh[0].h_all) most = std::max(most, v);
+  }
+  return most;
+}
+
+// Ship the winners of ranks [lo, lo + rows_cap) to their owners; rows_in is
+// derived on the device from the owner's new_count (no host round trip).
+static int move_rows(rtla_ctx* x, uint64_t lo) {
   const int G = x->nshard;
   const uint64_t rc = x->rows_cap, RW = (uint64_t)x->L.W + 2;
   auto part = [&](uint64_t n) { return n > lo ? std::min<uint64_t>(n - lo, rc) : 0; };
+  for (auto& s : x->sh) HIPCHK(launch_part_counts(s.new_count, G, lo, rc, s.rows_in, s.rows_base, s.ctr, x->stream));
   if (x->world == 1) {
-    for (auto& dst : x->sh) {
-      std::vector<uint64_t> in(G, 0);
+    for (auto& dst : x->sh)
       for (auto& src : x->sh) {
-        uint64_t n = part(src.h_new_out[dst.id]);
-        in[src.id] = n;
+        const uint64_t n = part(src.h_new_out[dst.id]);
         if (n)
           HIPCHK(hipMemcpyAsync(dst.recv_rows + (uint64_t)src.id * rc * RW, src.send_rows + (uint64_t)dst.id * rc * RW,
                                 4 * n * RW, hipMemcpyDeviceToDevice, x->stream));
       }
-      HIPCHK(hipMemcpyAsync(dst.rows_in, in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
-      HIPCHK(hipStreamSynchronize(x->stream));  // `in` is a host temporary
-    }
     return RTLA_OK;
   }
   Shard& s = x->sh[0];
-  std::vector<uint64_t> in(G, 0);
-  for (int p = 0; p < G; p++) in[p] = part(s.h_new_in[p]);
-  HIPCHK(hipMemcpyAsync(s.rows_in, in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
   NCCLCHK(ncclGroupStart());
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
-    NCCLCHK(ncclSend(s.send_rows + (uint64_t)p * rc * RW, part(s.h_new_out[p]) * RW, ncclUint32, p, x->comm,
-                     x->stream));
-    NCCLCHK(ncclRecv(s.recv_rows + (uint64_t)p * rc * RW, in[p] * RW, ncclUint32, p, x->comm, x->stream));
+    const uint64_t no = part(s.h_new_out[p]), ni = part(s.h_new_in[p]);
+    if (no) NCCLCHK(ncclSend(s.send_rows + (uint64_t)p * rc * RW, no * RW, ncclUint32, p, x->comm, x->stream));
+    if (ni) NCCLCHK(ncclRecv(s.recv_rows + (uint64_t)p * rc * RW, ni * RW, ncclUint32, p, x->comm, x->stream));
   }
   NCCLCHK(ncclGroupEnd());
-  HIPCHK(hipStreamSynchronize(x->stream));
   return RTLA_OK;
 }
 
@@ -659,11 +716,8 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
                          next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags()));
   } else {
     // lock-step chunks over the frontier; every shard runs the same number
-    uint64_t mx = 0;
-    for (auto& s : x->sh) mx = std::max(mx, s.n_cur);
-    int rc = allreduce_u64(x, &mx, 1, 1);
-    if (rc) return rc;
-    uint64_t rounds = (mx + x->chunk - 1) / x->chunk;
+    // (x->max_front = the largest frontier of any shard, from the last level's reduction)
+    const uint64_t rounds = std::max<uint64_t>(1, (x->max_front + x->chunk - 1) / x->chunk);
     for (uint64_t c = 0; c < rounds; c++) {
       for (size_t k = 0; k < x->sh.size(); k++) {
         Shard& s = x->sh[k];
@@ -674,43 +728,39 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
         uint64_t blocks = (e - b + 3) / 4;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), (uint64_t)x->grid);
         HIPCHK(launch_expand(L, s.front[s.cur], b, e, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[k],
-                             next_cap[k], s.table, x->tlog2, s.ctr, box, grid, x->stream));
-        HIPCHK(hipMemcpyAsync(s.h_out.data(), s.out_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+                             next_cap[k], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), s.sent));
       }
-      HIPCHK(hipStreamSynchronize(x->stream));
-      for (auto& s : x->sh)
-        for (int p = 0; p < G; p++)
-          if (s.h_out[p] > x->box_cap) {
-            report_flags(FLAG_OUTBOX_FULL);
-            x->finished = true;
-            return RTLA_E_OVERFLOW;
-          }
-      rc = exchange_fps(x);
+      int rc = gather_counts(x);
+      if (rc) return rc;
+      rc = move_fps(x);
       if (rc) return rc;
       for (auto& s : x->sh) {
         HIPCHK(hipMemsetAsync(s.new_count, 0, 8 * G, x->stream));
+        uint64_t mx_in = 0;
+        for (uint64_t v : s.h_in) mx_in = std::max(mx_in, v);
         HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_ans, s.new_count,
-                                    s.ctr, x->stream));
+                                    s.ctr, mx_in, x->stream));
       }
-      rc = exchange_answers(x);
+      rc = move_answers(x);
       if (rc) return rc;
-      uint64_t most = 0;
-      for (auto& s : x->sh)
-        for (int p = 0; p < G; p++) most = std::max(most, std::max(s.h_new_out[p], s.h_new_in[p]));
-      rc = allreduce_u64(x, &most, 1, 1);
-      if (rc) return rc;
+      const uint64_t most = most_winners(x);
       for (uint64_t lo = 0; lo < most; lo += x->rows_cap) {
         for (size_t k = 0; k < x->sh.size(); k++) {
           Shard& s = x->sh[k];
+          uint64_t mx_out = 0;
+          for (uint64_t v : s.h_out) mx_out = std::max(mx_out, v);
           HIPCHK(launch_pack_rows(L, s.front[s.cur], s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
-                                  x->box_cap, lo, lo + x->rows_cap, s.send_rows, x->rows_cap, s.ctr, x->stream));
+                                  x->box_cap, lo, lo + x->rows_cap, s.send_rows, x->rows_cap, s.ctr, mx_out,
+                                  x->stream));
         }
-        rc = exchange_rows(x, lo);
+        rc = move_rows(x, lo);
         if (rc) return rc;
         for (size_t k = 0; k < x->sh.size(); k++) {
           Shard& s = x->sh[k];
-          HIPCHK(launch_unpack_rows(L.W, s.recv_rows, s.rows_in, G, x->rows_cap, s.front[s.cur ^ 1], s.parents,
-                                    next_base[k], next_cap[k], s.ctr, x->stream));
+          uint64_t mx_rows = 0;
+          for (uint64_t v : s.h_new_in) mx_rows = std::max(mx_rows, v > lo ? std::min(v - lo, x->rows_cap) : 0);
+          HIPCHK(launch_unpack_rows(L.W, s.recv_rows, s.rows_in, s.rows_base, G, x->rows_cap, s.front[s.cur ^ 1],
+                                    s.parents, next_base[k], next_cap[k], s.ctr, mx_rows, x->stream));
         }
       }
     }
@@ -718,7 +768,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev1, x->stream));
   // gather counters
   uint64_t sums[4] = {0, 0, 0, 0};  // new, generated, probes, frontier
-  uint64_t maxs[3] = {0, 0, 0};     // flags, violation, device time (us)
+  uint64_t maxs[4] = {0, 0, 0, 0};  // flags, violation, device time (us), largest next frontier of a shard
   std::vector<DevCounters> hc(x->sh.size());
   for (size_t k = 0; k < x->sh.size(); k++)
     HIPCHK(hipMemcpyAsync(&hc[k], x->sh[k].ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, x->stream));
@@ -731,15 +781,15 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     maxs[0] |= (uint64_t)hc[k].flags;
     maxs[1] = std::max<uint64_t>(maxs[1], hc[k].viol_mask ? 1 : 0);
     maxs[2] = std::max<uint64_t>(maxs[2], (uint64_t)(kms * 1000.0));
+    maxs[3] = std::max<uint64_t>(maxs[3], hc[k].next_count);
     if (hc[k].viol_mask && !s.viol_mask) {
       s.viol_mask = hc[k].viol_mask; s.viol_in_model = hc[k].viol_in_model; s.viol_inst = hc[k].viol_inst;
       s.viol_parent = hc[k].viol_parent; s.viol_child = hc[k].viol_child;
     }
   }
-  int rc = allreduce_u64(x, sums, 4, 0);
+  int rc = allreduce2_u64(x, sums, 4, maxs, 4);
   if (rc) return rc;
-  rc = allreduce_u64(x, maxs, 3, 1);
-  if (rc) return rc;
+  x->max_front = maxs[3];
   if (maxs[0]) { report_flags((int)maxs[0]); x->finished = true; return flags_to_status((int)maxs[0]); }
   uint64_t nnew = sums[0];
   x->generated += sums[1];

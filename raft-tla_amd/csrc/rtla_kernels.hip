@@ -549,8 +549,10 @@ namespace {
 constexpr int RING = 128;   // pair ring (u16: state lane << 8 | instance - window base)
 constexpr int NEWCAP = 128; // new-state list (u64 parent records)
 
+constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
+
 __host__ __device__ constexpr int compact_lds_words(int W, int AW) {
-  return 64 * W + 64 * AW + RING / 2 + 2 * NEWCAP;
+  return 64 * W + 64 * AW + RING / 2 + 2 * NEWCAP + 4 * 8;  // + per-owner (base, used) of the open outbox chunk
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -599,6 +601,17 @@ __device__ __forceinline__ unsigned long long cand_mask(const Layout& L, const u
   return m;
 }
 
+// Zero records (fp 0:0, skipped by k_insert_remote) in outbox slots [from, to) of owner o.
+__device__ __forceinline__ void outbox_holes(const ShardBox& box, int o, unsigned long long from,
+                                             unsigned long long to, int lane) {
+  to = min(to, box.cap);
+  for (unsigned long long j = from + lane; j < to; j += 64) {
+    const unsigned long long k = (unsigned long long)o * box.cap + j;
+    box.send_fp[2 * k] = 0ull;
+    box.send_fp[2 * k + 1] = 0ull;
+  }
+}
+
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
   const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
   const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
@@ -610,12 +623,13 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #ifndef RTLA_COMPACT_WAVES_PER_EU
 #define RTLA_COMPACT_WAVES_PER_EU 1
 #endif
-template <int NS>
+template <int NS, bool MULTI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_COMPACT_WAVES_PER_EU)))
 k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
                  unsigned long long cur_base, unsigned long long* __restrict__ parents, unsigned long long next_base,
-                 unsigned long long next_cap, unsigned long long* table, int tlog2, DevCounters* ctr, int me,
-                 int xflags) {
+                 unsigned long long next_cap, unsigned long long* table, unsigned long long* sent, int tlog2,
+                 DevCounters* ctr, ShardBox box, int xflags) {
+  const int me = box.me;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -625,15 +639,28 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   const LaneWords pall_mine{rows + 64 * W + lane};
   uint16_t* ring = reinterpret_cast<uint16_t*>(rows + 64 * W + 64 * AW);
   unsigned long long* newl = reinterpret_cast<unsigned long long*>(rows + 64 * W + 64 * AW + RING / 2);
+  unsigned long long* obox = newl + NEWCAP;  // [o] = base of the open chunk, [8 + o] = slots used
+  if (MULTI) {
+    if (lane < 8) {
+      obox[lane] = ~0ull;
+      obox[8 + lane] = OBOX_CHUNK;
+    }
+    wave_sync();
+  }
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
 
   unsigned my_gen = 0, my_probe = 0;
   const int ninst = L.fam[F_COUNT];
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
-  // pending probe (issued by the previous chunk)
+  // pending probe (issued by the previous chunk).  MULTI: a successor owned
+  // by another shard probes this shard's SENT cache instead of the set: the
+  // first time this shard meets it, its (fingerprint, parent) record goes to
+  // the owner's outbox; later copies are dropped (the owner already has it).
   bool pend = false;
-  unsigned long long pold = 0, pkey = 0, pidx = 0, prec = 0;
+  unsigned long long pold = 0, pidx = 0, prec = 0;
+  FP pf{0, 0};
+  int powner = 0;
   int nnew = 0;  // entries in newl (uniform)
 
   auto flush_new = [&]() {
@@ -651,7 +678,43 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   };
   auto resolve = [&]() {
     bool isnew = false;
-    if (pend) isnew = fpset_resolve(table, tlog2, pkey, pidx, pold, ctr);
+    if (pend) isnew = fpset_resolve((MULTI && powner != me) ? sent : table, tlog2, pf.b | 1ull, pidx, pold, ctr);
+    if (MULTI) {  // records for other owners: one outbox reservation per (wave, owner)
+      const bool rem = isnew && powner != me;
+      isnew = isnew && powner == me;
+      unsigned long long om = wave_or_u64(rem ? 1ull << powner : 0ull);
+      while (om) {
+        const int o = __builtin_ctzll(om);
+        om &= om - 1;
+        const unsigned long long m = __ballot(rem && powner == o);
+        const int cnt = __popcll(m);
+        unsigned long long b = obox[o], used = obox[8 + o];
+        if (used + cnt > OBOX_CHUNK) {  // close the open chunk (holes = zero records), reserve the next
+          if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
+          unsigned long long nb = 0;
+          if (lane == 0) nb = atomicAdd(&box.out_count[o], (unsigned long long)OBOX_CHUNK);
+          b = shfl0_u64(nb);
+          used = 0;
+        }
+        if (rem && powner == o) {
+          const unsigned long long slot = b + used + __popcll(m & lanes_below);
+          if (slot < box.cap) {
+            const unsigned long long k = (unsigned long long)o * box.cap + slot;
+            box.send_fp[2 * k] = pf.a;
+            box.send_fp[2 * k + 1] = pf.b;
+            box.send_ref[k] = ((prec >> 16) & ((1ull << 40) - 1ull)) - cur_base << 16 | (prec & 0xffffull);
+          } else {
+            set_flag(ctr, FLAG_OUTBOX_FULL);
+          }
+        }
+        wave_sync();
+        if (lane == 0) {
+          obox[o] = b;
+          obox[8 + o] = used + cnt;
+        }
+        wave_sync();
+      }
+    }
     const unsigned long long m = __ballot(isnew);
     if (m) {
       if (isnew) newl[nnew + __popcll(m & lanes_below)] = prec;
@@ -749,14 +812,17 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
         }
         my_gen += en ? 1u : 0u;
         bool probe = false;
-        unsigned long long key = 0, idx = 0;
+        unsigned long long idx = 0;
+        FP cf{0, 0};
+        int owner = me;
         if (en && d.in_model) {
           const FP cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
                                                 : fp_add(qfp, delta_fp<NS>(L, prow, d));
           if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
             probe = !(xflags & XF_NO_PROBE);
-            key = cfp.b | 1ull;
+            cf = cfp;
             idx = cfp.a >> (64 - tlog2);
+            owner = MULTI ? fp_owner(cfp, box.nshard) : me;
           }
         }
         if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
@@ -783,10 +849,11 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
         if (probe) {
           my_probe++;
           pend = true;
-          pkey = key;
+          pf = cf;
           pidx = idx;
+          powner = owner;
           prec = (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
-          pold = atomicCAS(&table[idx], 0ull, key);
+          pold = atomicCAS(&((MULTI && owner != me) ? sent : table)[idx], 0ull, cf.b | 1ull);
         }
         done += cnt;
       }
@@ -795,6 +862,12 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   }
   resolve();
   if (nnew) flush_new();
+  if (MULTI) {
+    for (int o = 0; o < box.nshard; o++) {
+      const unsigned long long b = obox[o], used = obox[8 + o];
+      if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
+    }
+  }
   for (int off = 32; off > 0; off >>= 1) {
     my_gen += __shfl_down(my_gen, off);
     my_probe += __shfl_down(my_probe, off);
@@ -880,20 +953,36 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
                                 const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
                                 unsigned long long* table, int tlog2, uint32_t* __restrict__ ans,
                                 unsigned long long* __restrict__ new_count, DevCounters* ctr) {
-  unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
-  unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  unsigned long long probes = 0;
-  for (; i < (unsigned long long)nshard * cap; i += stride) {
-    unsigned long long p = i / cap, k = i - p * cap;
-    if (k >= counts[p]) continue;
-    FP f{recv_fp[2 * i], recv_fp[2 * i + 1]};
-    int r = fpset_insert(table, tlog2, f);
-    if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
-    ans[i] = r == 1 ? (uint32_t)atomicAdd(&new_count[p], 1ull) + 1u : 0u;
-    probes++;
+  // grid.y = source shard p; lanes of a wave share p, so one atomic per wave
+  // hands out the dense ranks of its new fingerprints
+  const unsigned long long p = blockIdx.y;
+  const unsigned long long n = counts[p];
+  const int lane = threadIdx.x & 63;
+  unsigned probes = 0;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long k0 = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); k0 < n;
+       k0 += stride) {
+    const unsigned long long k = k0 + lane;
+    int r = 0;
+    if (k < n) {
+      const unsigned long long i = p * cap + k;
+      const FP f{recv_fp[2 * i], recv_fp[2 * i + 1]};
+      if (f.a | f.b) {  // 0:0 = a hole in the sender's outbox chunk
+        r = fpset_insert(table, tlog2, f);
+        if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
+        probes++;
+      }
+    }
+    const unsigned long long m = __ballot(r == 1);
+    unsigned long long b = 0;
+    if (m) {
+      if (lane == 0) b = atomicAdd(&new_count[p], (unsigned long long)__popcll(m));
+      b = shfl0_u64(b);
+    }
+    if (k < n) ans[p * cap + k] = r == 1 ? (uint32_t)(b + __popcll(m & ((1ull << lane) - 1ull))) + 1u : 0u;
   }
   for (int off = 32; off > 0; off >>= 1) probes += __shfl_down(probes, off);
-  if ((threadIdx.x & 63) == 0 && probes) atomicAdd(&ctr->probes, probes);
+  if (lane == 0 && probes) atomicAdd(&ctr->probes, (unsigned long long)probes);
 }
 
 // Sender side: materialise the queued successors whose owner answered "new"
@@ -901,70 +990,139 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
 // RW = W + 2 words per slot).  Invariants are checked here, where parent and
 // action are known; a violation is recorded against the local parent.
 template <int NS>
-__global__ void k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base, int me,
-                            const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
-                            const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
-                            unsigned long long lo, unsigned long long hi, uint32_t* __restrict__ rows,
-                            unsigned long long rows_cap, DevCounters* ctr) {
-  unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
-  unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  const int RW = L.W + 2;
-  for (; i < (unsigned long long)nshard * cap; i += stride) {
-    unsigned long long p = i / cap, k = i - p * cap;
-    if (k >= counts[p]) continue;
-    unsigned long long a = ans[i];
-    if (a == 0 || a - 1 < lo || a - 1 >= hi) continue;
-    unsigned long long ref = send_ref[i];
-    unsigned long long s = ref >> 16;
-    int inst = (int)(ref & 0xffff);
-    const uint32_t* prow = cur + s * (unsigned long long)L.W;
-    Delta d;
-    compute_delta<NS>(L, prow, inst, d);
-    uint32_t* dst = rows + (p * rows_cap + (a - 1 - lo)) * (unsigned long long)RW;
-    // copy + patch first, then allLogs' straight into the destination row, then the fingerprint
-    materialize<NS>(L, prow, d, prow + L.off_all, FP{0, 0}, dst);
-    FP afp = alllogs_delta<NS>(L, prow, dst + L.off_all);
-    row_set_fp(dst, fp_add(fp_add(row_fp(prow), afp), delta_fp<NS>(L, prow, d)));
-    unsigned long long pr = (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
-    dst[L.W] = (uint32_t)pr;
-    dst[L.W + 1] = (uint32_t)(pr >> 32);
-    int code = cover_code(L, inst, d.sub);
-    atomicAdd(&ctr->cover[COVER_CODES + code], 1ull);
-    int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-    if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-      ctr->viol_parent = cur_base + s;
-      ctr->viol_inst = inst;
-      ctr->viol_in_model = 1;
-      ctr->viol_child = ~0ull;
+__global__ void __launch_bounds__(256)
+k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base, int me,
+            const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
+            const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap, unsigned long long lo,
+            unsigned long long hi, uint32_t* __restrict__ rows, unsigned long long rows_cap, DevCounters* ctr) {
+  // A wave scans 64 records of owner p (grid.y), compacts the winners of
+  // this sub-round, gathers their parent rows into LDS (one coalesced read
+  // per row), builds each successor in place and ships row + parent record
+  // to the slot the owner's answer names (one coalesced write per row).
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ unsigned int cov[COVER_CODES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int W = L.W, AW = L.all_words, RW = W + 2;
+  uint32_t* lrows = lds + wave * lane_lds_words(W, AW);
+  const LaneWords pall{lrows + 64 * W + lane};
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
+  __syncthreads();
+  const unsigned long long p = blockIdx.y;  // owner shard
+  const unsigned long long n = counts[p];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; k0 < n;
+       k0 += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const unsigned long long k = k0 + lane;
+    const unsigned long long i = p * cap + k;
+    const unsigned long long a = k < n ? ans[i] : 0ull;
+    const bool win = a != 0 && a - 1 >= lo && a - 1 < hi;
+    const unsigned long long m = __ballot(win);
+    if (!m) continue;
+    const int nw = __popcll(m);
+    // compact: winner number r of this wave = lane w_r
+    int r_of_lane = __popcll(m & below);
+    unsigned long long ref = win ? send_ref[i] : 0ull;
+    unsigned long long dslot = win ? a - 1 - lo : 0ull;
+    // lane r takes the r-th winner's (ref, dslot)
+    int src_lane = 0;
+    {
+      unsigned long long mm = m;
+      for (int r = 0; r < nw; r++) {
+        const int l = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        if (lane == r) src_lane = l;
+      }
     }
+    (void)r_of_lane;
+    ref = shfl_u64(ref, src_lane);
+    dslot = shfl_u64(dslot, src_lane);
+    const bool act = lane < nw;
+    const unsigned long long s = ref >> 16;
+    const int inst = (int)(ref & 0xffffull);
+    for (int r = 0; r < nw; r++) {
+      const unsigned long long sr = readlane_u64(s, r);
+      const uint32_t* src = cur + sr * (unsigned long long)W;
+      for (int w = lane; w < W; w += 64) lrows[r * W + w] = src[w];
+    }
+    wave_sync();
+    uint32_t* prow = lrows + lane * W;
+    if (act) {
+      const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
+      Delta d;
+      compute_delta<NS>(L, prow, inst, d);
+      const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
+      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+      if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+        ctr->viol_parent = cur_base + s;
+        ctr->viol_inst = inst;
+        ctr->viol_in_model = 1;
+        ctr->viol_child = ~0ull;
+      }
+      atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
+      materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
+    }
+    wave_sync();
+    for (int r = 0; r < nw; r++) {
+      const unsigned long long ds = readlane_u64(dslot, r);
+      uint32_t* dst = rows + (p * rows_cap + ds) * (unsigned long long)RW;
+      for (int w = lane; w < W; w += 64) dst[w] = lrows[r * W + w];
+      if (lane == 0) {
+        const unsigned long long pr =
+            (unsigned long long)me << 56 | (cur_base + readlane_u64(s, r)) << 16 | (unsigned long long)__builtin_amdgcn_readlane(inst, r);
+        dst[W] = (uint32_t)pr;
+        dst[W + 1] = (uint32_t)(pr >> 32);
+      }
+    }
+    wave_sync();
   }
+  __syncthreads();
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
+    if (cov[k]) atomicAdd(&ctr->cover[COVER_CODES + k], (unsigned long long)cov[k]);
 }
 
 // Owner side: append the received rows to the next frontier (one wave per
 // row, coalesced copy) with their cross-shard parent records.
 __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ counts,
-                              int nshard, unsigned long long rows_cap, uint32_t* __restrict__ next,
-                              unsigned long long* __restrict__ parents, unsigned long long next_base,
-                              unsigned long long next_cap, DevCounters* ctr) {
+                              const unsigned long long* __restrict__ bases, int nshard, unsigned long long rows_cap,
+                              uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
+                              unsigned long long next_base, unsigned long long next_cap, DevCounters* ctr) {
+  // grid.y = source shard p; its rows land at the contiguous slots bases[p] + k
+  // (bases from k_part_counts: no per-row atomics)
+  const unsigned long long p = blockIdx.y;
+  const unsigned long long n = counts[p], base = bases[p];
   const int lane = threadIdx.x & 63;
   const int RW = W + 2;
-  unsigned long long wv = (blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x) >> 6;
-  unsigned long long nw = ((unsigned long long)gridDim.x * blockDim.x) >> 6;
-  for (unsigned long long i = wv; i < (unsigned long long)nshard * rows_cap; i += nw) {
-    unsigned long long p = i / rows_cap, k = i - p * rows_cap;
-    if (k >= counts[p]) continue;
-    const uint32_t* src = rows + i * (unsigned long long)RW;
-    unsigned long long o = 0;
-    if (lane == 0) o = atomicAdd(&ctr->next_count, 1ull);
-    o = shfl0_u64(o);
+  const unsigned long long wv = (blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x) >> 6;
+  const unsigned long long nw = ((unsigned long long)gridDim.x * blockDim.x) >> 6;
+  for (unsigned long long k = wv; k < n; k += nw) {
+    const unsigned long long o = base + k;
     if (o >= next_cap) {
       if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
       continue;
     }
+    const uint32_t* src = rows + (p * rows_cap + k) * (unsigned long long)RW;
     uint32_t* dst = next + o * (unsigned long long)W;
     for (int w = lane; w < W; w += 64) dst[w] = src[w];
     if (lane == 0) parents[next_base + o] = (unsigned long long)src[W] | (unsigned long long)src[W + 1] << 32;
   }
+}
+
+// rows_in[p] = the part [lo, lo + rc) of the new_count[p] rows owner-side.
+// and bases[p] = the next-frontier slot of its first row; advances next_count.
+__global__ void k_part_counts(const unsigned long long* __restrict__ new_count, int nshard, unsigned long long lo,
+                              unsigned long long rc, unsigned long long* __restrict__ rows_in,
+                              unsigned long long* __restrict__ bases, DevCounters* ctr) {
+  if (threadIdx.x != 0) return;
+  unsigned long long b = ctr->next_count;
+  for (int p = 0; p < nshard; p++) {
+    const unsigned long long n = new_count[p];
+    const unsigned long long r = n > lo ? min(n - lo, rc) : 0ull;
+    rows_in[p] = r;
+    bases[p] = b;
+    b += r;
+  }
+  ctr->next_count = b;
 }
 
 // Insert the fingerprints of `n` rows (Init).  new_flags[i] = 1 if new.
@@ -1101,10 +1259,12 @@ int expand_blocks_per_cu(const Layout& L) {
 
 hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
                          uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
-                         int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags) {
+                         int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags,
+                         uint64_t* sent) {
   if (s_end <= s_begin) return hipSuccess;
   const int cwpb = expand_compact_wpb(L);
-  if (box.nshard == 1 && cwpb > 0 && !(xflags & XF_LANE_KERNEL)) {
+  if (cwpb > 0 && !(xflags & XF_LANE_KERNEL) && (box.nshard == 1 || sent)) {
+    const bool multi = box.nshard > 1;
     {  // k_materialize's range starts at the next-frontier count before this launch
       hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
                                     hipMemcpyDeviceToDevice, st);
@@ -1114,27 +1274,43 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
     const uint64_t groups = (s_end - s_begin + 63) / 64;
     uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
     if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
-      static int per_cu[2][NMAX + 1];
-      int& pc = per_cu[wpb == 1][L.N];
+      static int per_cu[2][2][NMAX + 1];
+      int& pc = per_cu[multi][wpb == 1][L.N];
       if (!pc) {
         const size_t l = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
         hipError_t e = hipErrorInvalidValue;
+#define RTLA_OCC(n) \
+  e = multi ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<n, true>, 64 * wpb, l) \
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<n, false>, 64 * wpb, l)
         switch (L.N) {
-          case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<1>, 64 * wpb, l); break;
-          case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<2>, 64 * wpb, l); break;
-          case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<3>, 64 * wpb, l); break;
-          case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<4>, 64 * wpb, l); break;
-          default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<5>, 64 * wpb, l); break;
+          case 1: RTLA_OCC(1); break;
+          case 2: RTLA_OCC(2); break;
+          case 3: RTLA_OCC(3); break;
+          case 4: RTLA_OCC(4); break;
+          default: RTLA_OCC(5); break;
         }
+#undef RTLA_OCC
         if (e != hipSuccess || pc < 1) pc = 16 / wpb;
       }
       blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * pc);
     }
     const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-    RTLA_DISPATCH_N(L, k_expand_compact, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur,
-                    (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base,
-                    (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,
-                    (unsigned long long*)table, tlog2, ctr, box.me, xflags);
+#define RTLA_COMPACT_CASE(n)                                                                                \
+  case n: {                                                                                                 \
+    auto kfn = multi ? k_expand_compact<n, true> : k_expand_compact<n, false>;                              \
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)s_begin, \
+                       (unsigned long long)s_end, (unsigned long long)cur_base, (unsigned long long*)parents,  \
+                       (unsigned long long)next_base, (unsigned long long)next_cap, (unsigned long long*)table, \
+                       (unsigned long long*)sent, tlog2, ctr, box, xflags);                                   \
+  } break;
+    switch (L.N) {
+      RTLA_COMPACT_CASE(1)
+      RTLA_COMPACT_CASE(2)
+      RTLA_COMPACT_CASE(3)
+      RTLA_COMPACT_CASE(4)
+      default: RTLA_COMPACT_CASE(5)
+    }
+#undef RTLA_COMPACT_CASE
     {
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -1192,37 +1368,51 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
   return hipGetLastError();
 }
 
+static unsigned grid_x(uint64_t n, int per_block) {
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + per_block - 1) / per_block, 4096));
+}
+
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
-                                hipStream_t st) {
-  uint64_t n = (uint64_t)nshard * cap;
-  uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_insert_remote, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned long long*)recv_fp,
-                     (const unsigned long long*)counts, nshard, (unsigned long long)cap, (unsigned long long*)table,
-                     tlog2, ans, (unsigned long long*)new_count, ctr);
+                                uint64_t max_count, hipStream_t st) {
+  if (!max_count) return hipSuccess;
+  hipLaunchKernelGGL(k_insert_remote, dim3(grid_x(max_count, 256), nshard), dim3(256), 0, st,
+                     (const unsigned long long*)recv_fp, (const unsigned long long*)counts, nshard,
+                     (unsigned long long)cap, (unsigned long long*)table, tlog2, ans, (unsigned long long*)new_count,
+                     ctr);
   return hipGetLastError();
 }
 
 hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_base, int me, const uint64_t* send_ref,
                             const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
-                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, hipStream_t st) {
-  uint64_t n = (uint64_t)nshard * cap;
-  uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-  RTLA_DISPATCH_N(L, k_pack_rows, dim3((unsigned)blocks), dim3(256), 0, st, L, cur, (unsigned long long)cur_base, me,
-                  (const unsigned long long*)send_ref, ans, (const unsigned long long*)counts, nshard,
-                  (unsigned long long)cap, (unsigned long long)lo, (unsigned long long)hi, rows,
-                  (unsigned long long)rows_cap, ctr);
+                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, uint64_t max_count,
+                            hipStream_t st) {
+  if (!max_count) return hipSuccess;
+  const int wpb = std::max(1, expand_lane_wpb(L));
+  const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+  RTLA_DISPATCH_N(L, k_pack_rows, dim3(grid_x(max_count, 64 * wpb), nshard), dim3(64 * wpb), lds, st, L, cur,
+                  (unsigned long long)cur_base, me, (const unsigned long long*)send_ref, ans,
+                  (const unsigned long long*)counts, nshard, (unsigned long long)cap, (unsigned long long)lo,
+                  (unsigned long long)hi, rows, (unsigned long long)rows_cap, ctr);
   return hipGetLastError();
 }
 
-hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, int nshard, uint64_t rows_cap,
-                              uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
-                              DevCounters* ctr, hipStream_t st) {
-  uint64_t waves = (uint64_t)nshard * rows_cap;
-  uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)blocks), dim3(256), 0, st, W, rows,
-                     (const unsigned long long*)counts, nshard, (unsigned long long)rows_cap, next,
-                     (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap, ctr);
+hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, const uint64_t* bases, int nshard,
+                              uint64_t rows_cap, uint32_t* next, uint64_t* parents, uint64_t next_base,
+                              uint64_t next_cap, DevCounters* ctr, uint64_t max_count, hipStream_t st) {
+  if (!max_count) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_rows, dim3(grid_x(max_count, 4), nshard), dim3(256), 0, st, W, rows,
+                     (const unsigned long long*)counts, (const unsigned long long*)bases, nshard,
+                     (unsigned long long)rows_cap, next, (unsigned long long*)parents, (unsigned long long)next_base,
+                     (unsigned long long)next_cap, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_part_counts(const uint64_t* new_count, int nshard, uint64_t lo, uint64_t rc, uint64_t* rows_in,
+                              uint64_t* bases, DevCounters* ctr, hipStream_t st) {
+  hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, (const unsigned long long*)new_count, nshard,
+                     (unsigned long long)lo, (unsigned long long)rc, (unsigned long long*)rows_in,
+                     (unsigned long long*)bases, ctr);
   return hipGetLastError();
 }
 
