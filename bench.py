@@ -29,11 +29,15 @@ sys.path.insert(0, os.path.join(ROOT, "raft-tla_amd"))
 # Feasible analogues of BASELINE.json configs (the reference's bounds give
 # >1e11 states): name -> (N, V, MaxTerm, MaxLogLen, MaxCopies, MaxInFlight, invariants)
 WORKLOADS = {
+    "raft3_v2_t2_l2_m2": (3, 2, 2, 2, 1, 2, ("ElectionSafety", "LogMatching")),
+    "raft3_v2_t2_l1_m3": (3, 2, 2, 1, 1, 3, ("ElectionSafety", "LogMatching")),
     "raft3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, ("ElectionSafety", "LogMatching")),
     "raft3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, ("NoTwoLeaders",)),
     "raft3_v1_t2_l1_m1": (3, 1, 2, 1, 1, 1, ("NoTwoLeaders",)),
 }
-DEFAULT = "raft3_v2_t2_l1_m2"
+DEFAULT = "raft3_v2_t2_l2_m2"
+# fingerprint-set size per workload (distinct states: 2.41e9, 2.54e9, 1.45e8)
+FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 32, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30}
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Random 8-B CAS into a table far beyond the 256 MiB Infinity Cache, all CUs:
 # measured on MI355X by tools/probe_calib.py (profiles/).
@@ -67,9 +71,10 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=12_000_000, help="states in the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--fpset-log2", type=int, default=30,
-                    help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 2^30 x 8 B = 8 GiB "
-                         "holds the bench model at 14%% load. 0 = auto (40%% of free HBM)")
+    ap.add_argument("--fpset-log2", type=int, default=0,
+                    help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the "
+                         "workload (2^32 slots = 32 GiB for the 2.4e9-state default at 56%% load, fewer per "
+                         "rank when sharded)")
     ap.add_argument("--levels", action="store_true", help="print the per-level table to stderr")
     ap.add_argument("--shards", type=int, default=0,
                     help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
@@ -90,7 +95,10 @@ def main():
 
     shape = WORKLOADS[args.workload]
     n, v, t, l, c, m, inv = shape
-    cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=args.fpset_log2, shards=args.shards,
+    fpl = args.fpset_log2 or FPSET_LOG2.get(args.workload, 30)
+    if not args.fpset_log2 and world > 1:  # each rank owns 1/world of the fingerprints
+        fpl = max(24, fpl - (world - 1).bit_length())
+    cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=fpl, shards=args.shards,
                       mem_budget=(200 << 30) if args.shards > 1 else 0)
     ck = rtla.Checker(cfg, rank=rank, world=world, comm_id=comm_id)
 
@@ -163,7 +171,7 @@ def main():
             "servers": n, "values": v, "max_term": t, "max_log": l, "max_copies": c, "max_in_flight": m,
             "invariants": list(inv), "distinct": distinct, "generated": generated, "depth": depth,
             "parallelism": "single" if world == 1 else "fp-sharded%d" % world,
-            "fpset_slots_log2": args.fpset_log2,
+            "fpset_slots_log2": fpl,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

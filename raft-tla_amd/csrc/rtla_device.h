@@ -17,6 +17,7 @@ enum {
   FLAG_FRONTIER_FULL = 4,   // next-frontier buffer too small
   FLAG_FPSET_FULL = 8,      // fingerprint set probe limit hit
   FLAG_OUTBOX_FULL = 16,    // exchange outbox region too small
+  FLAG_BAD_INDEX = 32,      // RTLA_CHECKED builds: a global index outside its buffer
 };
 
 // Fingerprint ownership across shards (ranks): low 32 bits of fp.a scaled to
@@ -62,6 +63,8 @@ struct DevCounters {
   unsigned long long viol_parent;
   unsigned long long viol_child;
   unsigned long long mat_begin;  // k_materialize: first next-frontier slot of the current expand launch
+  // buffer capacities (rows of the current / next frontier, parent records), for RTLA_CHECKED builds
+  unsigned long long cap_cur, cap_next, cap_parents;
   unsigned long long cover[2 * COVER_CODES];  // [0,C): generated, [C,2C): distinct
 };
 

@@ -81,6 +81,7 @@ struct Shard {
   uint32_t* recv_rows = nullptr;   // [G][rows_cap][W + 2]
   uint64_t* sent = nullptr;        // [2^tlog2] fingerprints this shard already sent to their owners
   std::vector<uint64_t> h_out, h_in, h_new_out, h_new_in, h_all;
+  uint64_t h_caps[3] = {0, 0, 0};  // -> DevCounters cap_cur / cap_next / cap_parents
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // violation found on this shard
   int viol_mask = 0, viol_in_model = 0, viol_inst = -1;
@@ -220,6 +221,7 @@ static void report_flags(int flags) {
   if (flags & FLAG_FRONTIER_FULL) fprintf(stderr, "rtla: next-frontier buffer full (raise frontier_cap / mem_budget)\n");
   if (flags & FLAG_FPSET_FULL) fprintf(stderr, "rtla: fingerprint set too full (raise fpset_log2)\n");
   if (flags & FLAG_OUTBOX_FULL) fprintf(stderr, "rtla: exchange outbox full (lower chunk)\n");
+  if (flags & FLAG_BAD_INDEX) fprintf(stderr, "rtla: checked build: a kernel index left its buffer\n");
 }
 
 // Run k_expand_batch on device rows; results copied to host, sorted by (input, instance).
@@ -702,6 +704,8 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   for (size_t k = 0; k < x->sh.size(); k++) {
     Shard& s = x->sh[k];
     HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
+    s.h_caps[0] = x->front_cap; s.h_caps[1] = x->front_cap; s.h_caps[2] = s.parents_cap;
+    HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
     next_base[k] = s.cur_base + s.n_cur;
     if (next_base[k] >= s.parents_cap) return RTLA_E_OVERFLOW;
     next_cap[k] = std::min<uint64_t>(x->front_cap, s.parents_cap - next_base[k]);

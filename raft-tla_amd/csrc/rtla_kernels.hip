@@ -59,6 +59,15 @@ __device__ __forceinline__ int fpset_insert(unsigned long long* table, int log2,
 
 __device__ __forceinline__ void set_flag(DevCounters* c, int f) { atomicOr(&c->flags, f); }
 
+// RTLA_CHECKED builds: every global row / parent-record index is checked
+// against the buffer capacities the host stores in DevCounters; a bad index
+// raises FLAG_BAD_INDEX (reported by rtla_step) instead of faulting.
+#ifdef RTLA_CHECKED
+#define RTLA_IDX_OK(ctr, idx, cap) ((idx) < (cap) ? true : (set_flag((ctr), FLAG_BAD_INDEX), false))
+#else
+#define RTLA_IDX_OK(ctr, idx, cap) true
+#endif
+
 // Finish an insert whose first CAS (at home slot `idx`) returned `old`:
 // continue linear probing while the slot holds another key.  true = new.
 __device__ __forceinline__ bool fpset_resolve(unsigned long long* table, int log2, unsigned long long key,
@@ -457,8 +466,8 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
       if (total) {
         if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)total);
         obase = shfl0_u64(obase);
-        write_new = obase + total <= next_cap;
-        if (!write_new && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+        write_new = true;  // slots < next_cap are written below, the rest dropped (flagged)
+        if (obase + total > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
       }
       unsigned long long robase[8];
       int roff[8];
@@ -487,8 +496,10 @@ k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_b
           todo &= todo - 1;
           if (newm >> bit & 1ull) {
             const int inst = wave_inst(L, base + bit, fixed, kmax);
-            parents[next_base + obase + off + k_new++] =
-                (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
+            const unsigned long long slot = obase + off + k_new++;
+            if (slot < next_cap)
+              parents[next_base + slot] =
+                  (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
           }
         }
       }
@@ -668,11 +679,12 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
     unsigned long long obase = 0;
     if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)nnew);
     obase = shfl0_u64(obase);
-    if (obase + nnew > next_cap) {
-      if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
-    } else {
-      for (int k = lane; k < nnew; k += 64) parents[next_base + obase + k] = newl[k];
-    }
+    // Slots past next_cap are dropped (and flagged); the ones below it are
+    // always written, so k_materialize never reads an unwritten record.
+    if (obase + nnew > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    for (int k = lane; k < nnew; k += 64)
+      if (obase + k < next_cap && RTLA_IDX_OK(ctr, next_base + obase + k, ctr->cap_parents))
+        parents[next_base + obase + k] = newl[k];
     wave_sync();
     nnew = 0;
   };
@@ -731,7 +743,8 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
     {
       const uint32_t* src = cur + s0 * (unsigned long long)W;
       const int nw = nvalid * W;
-      for (int w = lane; w < nw; w += 64) rows[w] = src[w];
+      if (RTLA_IDX_OK(ctr, s0 + nvalid, ctr->cap_cur + 1))
+        for (int w = lane; w < nw; w += 64) rows[w] = src[w];
     }
     wave_sync();
     const bool valid = lane < nvalid;
@@ -907,14 +920,16 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
     const int nv = (int)min<unsigned long long>(64ull, end - g);
     const unsigned long long slot = g + lane;
     const bool act = lane < nv;
-    const unsigned long long pr = act ? parents[next_base + slot] : 0ull;
+    const unsigned long long pr =
+        act && RTLA_IDX_OK(ctr, next_base + slot, ctr->cap_parents) ? parents[next_base + slot] : 0ull;
     const unsigned long long sidx = ((pr >> 16) & ((1ull << 40) - 1ull)) - cur_base;
     const int inst = (int)(pr & 0xffffull);
     // gather the parent rows: one coalesced row read per slot (rows stay in L2)
     for (int r = 0; r < nv; r++) {
       const unsigned long long sr = readlane_u64(sidx, r);
       const uint32_t* src = cur + sr * (unsigned long long)W;
-      for (int w = lane; w < W; w += 64) rows[r * W + w] = src[w];
+      if (RTLA_IDX_OK(ctr, sr, ctr->cap_cur))
+        for (int w = lane; w < W; w += 64) rows[r * W + w] = src[w];
     }
     wave_sync();
     if (act) {
@@ -936,7 +951,8 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
     {  // the group's rows are contiguous in the next frontier: coalesced stores
       uint32_t* dst = next + g * (unsigned long long)W;
       const int nw = nv * W;
-      for (int w = lane; w < nw; w += 64) dst[w] = rows[w];
+      if (RTLA_IDX_OK(ctr, g + nv, ctr->cap_next + 1))
+        for (int w = lane; w < nw; w += 64) dst[w] = rows[w];
     }
     wave_sync();
   }

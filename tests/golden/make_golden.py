@@ -32,6 +32,12 @@ CASES = {
     "n3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, (NTL,), False, True),
     "n3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, (ES, LM), False, True),
 }
+# Models too large for the CPU oracle to exhaust here: a bounded prefix of
+# complete BFS levels (the oracle stops after the first level that passes
+# max_distinct).  name: (N, V, T, L, C, M, invariants, max_distinct)
+PREFIXES = {
+    "n3_v2_t2_l2_m2_prefix": (3, 2, 2, 2, 1, 2, (ES, LM), 60_000_000),
+}
 
 
 def main():
@@ -62,6 +68,17 @@ def main():
             case["source"] += " + oracle/raft_values.py"
         out[name] = case
         print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
+    for name, (n, v, t, l, c, m, inv, cap) in PREFIXES.items():
+        if not big:
+            continue
+        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8)
+        assert r["rc"] in (0, -4), (name, r["rc"])
+        out[name] = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
+                     "invariants": list(inv), "prefix": True, "levels": r["levels"],
+                     "distinct": r["distinct"], "generated": r["generated"],
+                     "source": "oracle/raft_cpu.c, first %d complete levels" % len(r["levels"])}
+        print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

@@ -22,7 +22,7 @@ import rtla
 pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bfs_counts.json")))
-SMALL = sorted(k for k, v in GOLD.items() if v["distinct"] < 3_000_000)
+SMALL = sorted(k for k, v in GOLD.items() if v["distinct"] < 3_000_000 and not v.get("prefix"))
 HASHED = sorted(k for k, v in GOLD.items() if "level_text_hash" in v)
 
 
@@ -158,7 +158,8 @@ def test_coverage_sums_to_generated():
     assert sum(cov[f][1] for f in fam) == res.distinct - 1
 
 
-BIG = sorted(k for k, v in GOLD.items() if v["distinct"] >= 3_000_000)
+BIG = sorted(k for k, v in GOLD.items() if v["distinct"] >= 3_000_000 and not v.get("prefix"))
+PREFIX = sorted(k for k, v in GOLD.items() if v.get("prefix"))
 
 
 @pytest.mark.parametrize("name", BIG)
@@ -167,6 +168,31 @@ def test_full_size_counts_match_golden(name):
     res = rtla.check(cfg_of(g, fpset_log2=(g["distinct"] * 3).bit_length()), trace=False)
     assert [[lv.new, lv.generated] for lv in res.levels] == g["levels"]
     assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+
+
+@pytest.mark.parametrize("name", PREFIX)
+def test_prefix_levels_match_golden(name):
+    """Models too large for the CPU oracle (the bench model is one): the
+    first complete BFS levels the oracle could afford must match exactly."""
+    g = GOLD[name]
+    with rtla.Checker(cfg_of(g, fpset_log2=30)) as ck:
+        ck.init()
+        while len(ck.levels) < len(g["levels"]):
+            assert ck.step() == rtla.OK
+        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
+
+
+def test_bench_model_full_size_sharding_invariant():
+    """At the bench model's full size (2.4e9 states, beyond the CPU oracle):
+    the search split into 2 fingerprint-owned shards (the multi-GPU exchange
+    protocol) must reproduce the single-shard per-level counts exactly."""
+    base = dict(n_server=3, n_value=2, max_term=2, max_log=2, max_copies=1, max_msgs=2,
+                invariants=("ElectionSafety", "LogMatching"))
+    one = rtla.check(rtla.Config(**base, fpset_log2=32), trace=False)
+    two = rtla.check(rtla.Config(**base, fpset_log2=31, shards=2, mem_budget=220 << 30), trace=False)
+    assert one.violation is None and two.violation is None
+    assert [[lv.new, lv.generated] for lv in two.levels] == [[lv.new, lv.generated] for lv in one.levels]
+    assert one.distinct > 2_000_000_000
 
 
 def test_fpset_probe_bench_inserts_all():
