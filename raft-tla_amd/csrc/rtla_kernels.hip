@@ -41,6 +41,39 @@ __device__ __forceinline__ unsigned long long shfl0_u64(unsigned long long v) {
   return (unsigned long long)lo | (unsigned long long)hi << 32;
 }
 
+// Copy n contiguous words global -> LDS with 8 loads in flight per lane
+// (a plain loop waits for every load before its LDS store).
+__device__ __forceinline__ void copy_words_lds(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, int n,
+                                               int lane) {
+  int w = lane;
+  for (; w + 7 * 64 < n; w += 8 * 64) {
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = src[w + j * 64];
+#pragma unroll
+    for (int j = 0; j < 8; j++) dst[w + j * 64] = v[j];
+  }
+  for (; w < n; w += 64) dst[w] = src[w];
+}
+
+// Gather nv rows of W words (row r from src_row(r), a wave-uniform address)
+// into LDS rows dst + r * W, 8 rows in flight.  W <= 64: one word per lane.
+template <class F>
+__device__ __forceinline__ void gather_rows_lds(uint32_t* __restrict__ dst, int W, int nv, F src_row, int lane) {
+  if (W <= 64) {
+    for (int r0 = 0; r0 < nv; r0 += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = (r0 + j < nv && lane < W) ? src_row(r0 + j)[lane] : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (r0 + j < nv && lane < W) dst[(r0 + j) * W + lane] = v[j];
+    }
+  } else {
+    for (int r = 0; r < nv; r++) copy_words_lds(dst + r * W, src_row(r), W, lane);
+  }
+}
+
 // Insert into the fingerprint set.  1 = newly inserted, 0 = already present,
 // -1 = probe limit exceeded (set too full).  Slots only ever change 0 -> key;
 // the CAS both tests and claims a slot, so every probe is one round trip.
@@ -743,8 +776,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
     {
       const uint32_t* src = cur + s0 * (unsigned long long)W;
       const int nw = nvalid * W;
-      if (RTLA_IDX_OK(ctr, s0 + nvalid, ctr->cap_cur + 1))
-        for (int w = lane; w < nw; w += 64) rows[w] = src[w];
+      if (RTLA_IDX_OK(ctr, s0 + nvalid, ctr->cap_cur + 1)) copy_words_lds(rows, src, nw, lane);
     }
     wave_sync();
     const bool valid = lane < nvalid;
@@ -925,12 +957,10 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
     const unsigned long long sidx = ((pr >> 16) & ((1ull << 40) - 1ull)) - cur_base;
     const int inst = (int)(pr & 0xffffull);
     // gather the parent rows: one coalesced row read per slot (rows stay in L2)
-    for (int r = 0; r < nv; r++) {
+    gather_rows_lds(rows, W, nv, [&](int r) {
       const unsigned long long sr = readlane_u64(sidx, r);
-      const uint32_t* src = cur + sr * (unsigned long long)W;
-      if (RTLA_IDX_OK(ctr, sr, ctr->cap_cur))
-        for (int w = lane; w < W; w += 64) rows[r * W + w] = src[w];
-    }
+      return cur + (RTLA_IDX_OK(ctr, sr, ctr->cap_cur) ? sr : 0ull) * (unsigned long long)W;
+    }, lane);
     wave_sync();
     if (act) {
       const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
@@ -1056,11 +1086,7 @@ k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_b
     const bool act = lane < nw;
     const unsigned long long s = ref >> 16;
     const int inst = (int)(ref & 0xffffull);
-    for (int r = 0; r < nw; r++) {
-      const unsigned long long sr = readlane_u64(s, r);
-      const uint32_t* src = cur + sr * (unsigned long long)W;
-      for (int w = lane; w < W; w += 64) lrows[r * W + w] = src[w];
-    }
+    gather_rows_lds(lrows, W, nw, [&](int r) { return cur + readlane_u64(s, r) * (unsigned long long)W; }, lane);
     wave_sync();
     uint32_t* prow = lrows + lane * W;
     if (act) {

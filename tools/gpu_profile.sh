@@ -5,7 +5,7 @@ set -u
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/prof
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-W=${WORKLOAD:-raft3_v2_t2_l1_m2}
+W=${WORKLOAD:-raft3_v2_t2_l2_m2}
 run() {  # name, limit, cmd...
   local name=$1 lim=$2; shift 2
   echo "== $name"; timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
