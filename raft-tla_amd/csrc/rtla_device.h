@@ -49,6 +49,7 @@ enum {
   XF_GENERIC_DELTA = 128, // compact kernel: never use the per-family specialised evaluation
   XF_BLOCK4 = 256,        // compact kernel: 4-wave workgroups instead of 1
   XF_NO_PERSIST = 512,    // compact kernel: one group per wave instead of persistent waves
+  XF_CAS_ONLY = 1024,     // compact kernel: probe with CAS only (no load-first)
 };
 
 // Per-level device counters (zeroed before each level except `cover`).

@@ -463,7 +463,7 @@ static int env_xflags() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RTLA_XFLAGS");
-    v = e ? (atoi(e) & (XF_LANE_KERNEL | XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST)) : 0;
+    v = e ? (atoi(e) & (XF_LANE_KERNEL | XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY)) : 0;
   }
   return v;
 }

@@ -92,6 +92,30 @@ __device__ __forceinline__ int fpset_insert(unsigned long long* table, int log2,
 
 __device__ __forceinline__ void set_flag(DevCounters* c, int f) { atomicOr(&c->flags, f); }
 
+// Finish an insert whose home slot `idx` was READ (not CAS'd) as `seen`.
+// Slots only ever change 0 -> key, so a slot holding the key proves the
+// state is present, and one holding another key can be skipped for good;
+// only an empty slot needs the CAS (which may then find the key after all).
+__device__ __forceinline__ bool fpset_resolve_loaded(unsigned long long* table, int log2, unsigned long long key,
+                                                     unsigned long long idx, unsigned long long seen,
+                                                     DevCounters* ctr) {
+  const unsigned long long mask = (1ull << log2) - 1ull;
+  for (int probe = 1;; probe++) {
+    if (seen == key) return false;
+    if (seen == 0ull) {
+      seen = atomicCAS(&table[idx], 0ull, key);
+      if (seen == 0ull) return true;
+      if (seen == key) return false;
+    }
+    if (probe >= 4096) {
+      set_flag(ctr, FLAG_FPSET_FULL);
+      return false;
+    }
+    idx = (idx + 1ull) & mask;
+    seen = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // RTLA_CHECKED builds: every global row / parent-record index is checked
 // against the buffer capacities the host stores in DevCounters; a bad index
 // raises FLAG_BAD_INDEX (reported by rtla_step) instead of faulting.
@@ -723,7 +747,11 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   };
   auto resolve = [&]() {
     bool isnew = false;
-    if (pend) isnew = fpset_resolve((MULTI && powner != me) ? sent : table, tlog2, pf.b | 1ull, pidx, pold, ctr);
+    if (pend) {
+      unsigned long long* t = (MULTI && powner != me) ? sent : table;
+      isnew = (xflags & XF_CAS_ONLY) ? fpset_resolve(t, tlog2, pf.b | 1ull, pidx, pold, ctr)
+                                     : fpset_resolve_loaded(t, tlog2, pf.b | 1ull, pidx, pold, ctr);
+    }
     if (MULTI) {  // records for other owners: one outbox reservation per (wave, owner)
       const bool rem = isnew && powner != me;
       isnew = isnew && powner == me;
@@ -898,7 +926,12 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
           pidx = idx;
           powner = owner;
           prec = (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
-          pold = atomicCAS(&((MULTI && owner != me) ? sent : table)[idx], 0ull, cf.b | 1ull);
+          unsigned long long* slotp = &((MULTI && owner != me) ? sent : table)[idx];
+          // load first: most successors are already in the set, and a plain
+          // load is cheaper than an atomic at the memory side; the CAS is
+          // only issued (at resolve time) when the home slot reads empty
+          pold = (xflags & XF_CAS_ONLY) ? atomicCAS(slotp, 0ull, cf.b | 1ull)
+                                        : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         done += cnt;
       }
