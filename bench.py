@@ -39,9 +39,31 @@ DEFAULT = "raft3_v2_t2_l2_m2"
 # fingerprint-set size per workload (distinct states: 2.41e9, 2.54e9, 1.45e8)
 FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 32, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30}
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-# Random 8-B CAS into a table far beyond the 256 MiB Infinity Cache, all CUs:
-# measured on MI355X by tools/probe_calib.py (profiles/).
-CAS_CEILING_PER_S = 2.0e10
+# Random 8-byte fingerprint-set accesses into a 32 GiB table (far beyond the
+# 256 MiB Infinity Cache), all CUs, measured on MI355X by tools/probe_calib.py
+# (profiles/r01_v5/calib.log): CAS ~1.55e10/s (insert or
+# present), load of a present key ~4.66e10/s.  The probe kernel loads the home
+# slot and CASes only empty slots, so its ceiling for P probes of which D
+# find new states is P / (P / LOAD + D / CAS).
+CAS_PER_S = 1.55e10
+LOAD_PER_S = 4.66e10
+
+
+def load_traffic(workload, launches):
+    """HBM bytes of the probe kernel per launch from the committed PMC profile
+    (profiles/*/traffic.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this workload), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("workload") == workload and t.get("kernel") == "k_expand_compact":
+            best = t
+            best["source"] = os.path.relpath(f, ROOT)
+    return best
 
 
 def dist_env():
@@ -138,20 +160,30 @@ def main():
     per_step = elapsed / args.steps
     value = distinct / per_step
 
-    # roofline of the dominant kernel (k_expand), from the last run's HIP-event times
+    # Roofline of the dominant kernel, the probe kernel k_expand_compact, from
+    # the last run's HIP-event times (expand_ms: the probe kernel alone; the
+    # rest of kernel_ms is k_materialize building the new rows).
+    # Algorithmic bytes of one launch over E frontier states: E*S (rows read)
+    # + P*64 (one 64-B HBM transaction per fingerprint-set probe, P in-model
+    # successors that differ from their parent) + D*8 (parent records).
     S = levels[0].row_bytes
-    kms = sum(lv.kernel_ms for lv in runs[-1][1:])
-    launches = len(runs[-1]) - 1
-    E = sum(lv.frontier for lv in levels[1:])
-    D = sum(lv.new for lv in levels[1:])
-    P = sum(lv.probes for lv in levels[1:])
-    stream_bytes = E * S + D * (S + 8)
-    probe_bytes = P * 64
-    achieved = (stream_bytes + probe_bytes) / (kms / 1e3) / 1e9
+    lv1 = levels[1:]
+    launches = len(lv1)
+    ems = sum(lv.expand_ms for lv in lv1)
+    kms = sum(lv.kernel_ms for lv in lv1)
+    E = sum(lv.frontier for lv in lv1)
+    D = sum(lv.new for lv in lv1)
+    P = sum(lv.probes for lv in lv1)
+    probe_kernel_bytes = E * S + P * 64 + D * 8
+    achieved = probe_kernel_bytes / world / (ems / 1e3) / 1e9   # per GPU
+    mat_ms = kms - ems
+    mat_bytes = D * (2 * S + 8)  # parent row read + record read + row written
+    traffic = load_traffic(args.workload, launches) if world == 1 else None
+    ra_ceiling = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
     if args.levels and rank == 0:
         for lv in levels:
-            print("level %3d frontier %12d new %12d generated %13d kernel %9.3f ms" %
-                  (lv.level, lv.frontier, lv.new, lv.generated, lv.kernel_ms), file=sys.stderr)
+            print("level %3d frontier %12d new %12d generated %13d kernel %9.3f ms (probe %9.3f ms)" %
+                  (lv.level, lv.frontier, lv.new, lv.generated, lv.kernel_ms, lv.expand_ms), file=sys.stderr)
 
     out = {
         "metric": "distinct states/sec (whole node) + wall time to exhaust, 3-server Raft",
@@ -175,15 +207,20 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "k_expand", "launches": launches, "kernel_ms_total": kms,
-            "kernel_ms_avg": kms / max(1, launches),
-            "algorithmic_bytes": stream_bytes + probe_bytes,
-            "model": "E*S + D*(S+8) streamed + one 64-B transaction per fingerprint probe",
-            "probes_per_s": P / (kms / 1e3),
-            "random_access": {"probes_per_s": P / (kms / 1e3), "ceiling_per_s": CAS_CEILING_PER_S,
-                              "frac": P / (kms / 1e3) / CAS_CEILING_PER_S,
-                              "source": "tools/probe_calib.py (random 8-B CAS, 8-32 GiB tables)"},
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "traffic_source": traffic["source"] if traffic else None,
+            "kernel": "k_expand_compact", "launches": launches, "kernel_ms_total": ems,
+            "kernel_ms_avg": ems / max(1, launches),
+            "bytes_per_launch": probe_kernel_bytes / max(1, launches),
+            "bytes_per_frontier_state": probe_kernel_bytes / max(1, E),
+            "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + 8 B per new parent record",
+            "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
+                              "frac": P / world / (ems / 1e3) / ra_ceiling,
+                              "model": "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S)",
+                              "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)"},
+            "k_materialize": {"ms_total": mat_ms, "bytes": mat_bytes,
+                              "GB_per_s": mat_bytes / world / (mat_ms / 1e3) / 1e9 if mat_ms > 0 else None},
         },
         "cpu_baseline": None,
     }

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 1
+#define RTLA_ABI_VERSION 2
 
 /* status codes */
 #define RTLA_OK 0
@@ -95,6 +95,7 @@ typedef struct {
     double kernel_ms;         /* k_expand time of this level (HIP events on the context's stream) */
     uint64_t probes;          /* in-model successors (fingerprint-set probes) */
     uint64_t row_bytes;       /* bytes of one packed state row */
+    double expand_ms;         /* of kernel_ms: the probe kernel alone (one shard); the rest builds the rows */
 } rtla_level_stats;
 
 /* Library / context lifetime.  world > 1: `comm_id` is the 128-byte RCCL
@@ -146,6 +147,10 @@ int rtla_time_expand(rtla_ctx *ctx, int xflags, int reps, double *ms);
 /* Calibration: n random 8-byte CAS inserts into a table of 2^log2 slots;
  * returns device seconds. */
 int rtla_probe_bench(int log2, uint64_t n, double *seconds, uint64_t *inserted);
+/* n random keys inserted (CAS, all new), then re-probed (all present) with a
+ * CAS and with the kernel's load-first protocol; device seconds of each pass. */
+int rtla_probe_bench2(int log2, uint64_t n, double *s_insert, double *s_seen_cas, double *s_seen_load,
+                      uint64_t *inserted);
 
 #ifdef __cplusplus
 }

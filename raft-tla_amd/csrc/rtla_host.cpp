@@ -82,7 +82,7 @@ struct Shard {
   uint64_t* sent = nullptr;        // [2^tlog2] fingerprints this shard already sent to their owners
   std::vector<uint64_t> h_out, h_in, h_new_out, h_new_in, h_all;
   uint64_t h_caps[3] = {0, 0, 0};  // -> DevCounters cap_cur / cap_next / cap_parents
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   // violation found on this shard
   int viol_mask = 0, viol_in_model = 0, viol_inst = -1;
   uint64_t viol_parent = 0, viol_child = ~0ull;
@@ -306,6 +306,7 @@ static void free_shard(Shard& s) {
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
+  if (s.evm) (void)hipEventDestroy(s.evm);
   s = Shard();
 }
 
@@ -367,6 +368,7 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
   HIPCHK(hipEventCreate(&s.ev0));
   HIPCHK(hipEventCreate(&s.ev1));
+  HIPCHK(hipEventCreate(&s.evm));
   return RTLA_OK;
 }
 
@@ -716,8 +718,9 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
     uint64_t blocks = (s.n_cur + 3) / 4;
     int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
+    HIPCHK(hipEventRecord(s.evm, x->stream));  // (re-recorded between the kernels when k_materialize runs)
     HIPCHK(launch_expand(L, s.front[s.cur], 0, s.n_cur, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[0],
-                         next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags()));
+                         next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), nullptr, s.evm));
   } else {
     // lock-step chunks over the frontier; every shard runs the same number
     // (x->max_front = the largest frontier of any shard, from the last level's reduction)
@@ -773,14 +776,18 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   // gather counters
   uint64_t sums[4] = {0, 0, 0, 0};  // new, generated, probes, frontier
   uint64_t maxs[4] = {0, 0, 0, 0};  // flags, violation, device time (us), largest next frontier of a shard
+  double emax = 0.0;  // probe-kernel (k_expand_*) time of this level, ms
   std::vector<DevCounters> hc(x->sh.size());
   for (size_t k = 0; k < x->sh.size(); k++)
     HIPCHK(hipMemcpyAsync(&hc[k], x->sh[k].ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   for (size_t k = 0; k < x->sh.size(); k++) {
     Shard& s = x->sh[k];
-    float kms = 0.f;
+    float kms = 0.f, ems = 0.f;
     (void)hipEventElapsedTime(&kms, s.ev0, s.ev1);
+    if (G == 1) (void)hipEventElapsedTime(&ems, s.ev0, s.evm);
+    else ems = kms;  // multi-shard: rows are built inside the exchange rounds
+    emax = std::max(emax, (double)ems);
     sums[0] += hc[k].next_count; sums[1] += hc[k].generated; sums[2] += hc[k].probes; sums[3] += s.n_cur;
     maxs[0] |= (uint64_t)hc[k].flags;
     maxs[1] = std::max<uint64_t>(maxs[1], hc[k].viol_mask ? 1 : 0);
@@ -818,6 +825,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     st->level = x->level; st->status = status; st->frontier = sums[3]; st->new_states = nnew;
     st->generated = sums[1]; st->distinct_total = x->distinct; st->generated_total = x->generated;
     st->kernel_ms = maxs[2] / 1000.0; st->probes = sums[2]; st->row_bytes = (uint64_t)L.W * 4;
+    st->expand_ms = x->world > 1 ? st->kernel_ms : emax;
     st->seconds = now_s() - t0;
   }
   return status;
@@ -984,6 +992,42 @@ extern "C" int rtla_time_expand(rtla_ctx* x, int xflags, int reps, double* ms) {
     total += m;
   }
   *ms = total / reps;
+  return RTLA_OK;
+}
+
+// Calibration of the fingerprint-set probe: n random keys inserted (all new,
+// CAS), then the same n keys probed again (all present) with a CAS and with
+// the load-first protocol the BFS kernel uses.  Device seconds of each pass.
+extern "C" int rtla_probe_bench2(int log2, uint64_t n, double* s_insert, double* s_seen_cas, double* s_seen_load,
+                                 uint64_t* inserted) {
+  uint64_t* table = nullptr;
+  DevCounters* ctr = nullptr;
+  HIPCHK(hipMalloc(&table, 8ull << log2));
+  HIPCHK(hipMalloc(&ctr, sizeof(DevCounters)));
+  HIPCHK(hipMemset(table, 0, 8ull << log2));
+  HIPCHK(hipMemset(ctr, 0, sizeof(DevCounters)));
+  hipEvent_t e[4];
+  for (auto& v : e) HIPCHK(hipEventCreate(&v));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipEventRecord(e[0], nullptr));
+  HIPCHK(launch_probe_bench(table, log2, n, 777, ctr, nullptr, 0));
+  HIPCHK(hipEventRecord(e[1], nullptr));
+  HIPCHK(launch_probe_bench(table, log2, n, 777, ctr, nullptr, 0));
+  HIPCHK(hipEventRecord(e[2], nullptr));
+  HIPCHK(launch_probe_bench(table, log2, n, 777, ctr, nullptr, 1));
+  HIPCHK(hipEventRecord(e[3], nullptr));
+  HIPCHK(hipEventSynchronize(e[3]));
+  float ms[3] = {0, 0, 0};
+  for (int k = 0; k < 3; k++) HIPCHK(hipEventElapsedTime(&ms[k], e[k], e[k + 1]));
+  DevCounters h;
+  HIPCHK(hipMemcpy(&h, ctr, sizeof h, hipMemcpyDeviceToHost));
+  if (s_insert) *s_insert = ms[0] / 1e3;
+  if (s_seen_cas) *s_seen_cas = ms[1] / 1e3;
+  if (s_seen_load) *s_seen_load = ms[2] / 1e3;
+  if (inserted) *inserted = h.next_count;  // the two re-probe passes insert nothing
+  for (auto& v : e) (void)hipEventDestroy(v);
+  (void)hipFree(table);
+  (void)hipFree(ctr);
   return RTLA_OK;
 }
 

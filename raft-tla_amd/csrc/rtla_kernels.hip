@@ -1275,13 +1275,19 @@ k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n
 // Microbenchmark kernel: random 8-B CAS inserts into a table (calibrates the
 // random-access roofline of the fingerprint set).
 __global__ void k_probe_bench(unsigned long long* table, int tlog2, unsigned long long n, unsigned long long seed,
-                              DevCounters* ctr) {
+                              DevCounters* ctr, int load_first) {
   unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
   unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   unsigned long long got = 0;
   for (; i < n; i += stride) {
     FP f = hash_u64(seed, i);
-    got += fpset_insert(table, tlog2, f) == 1;
+    if (load_first) {
+      const unsigned long long idx = f.a >> (64 - tlog2);
+      const unsigned long long v = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      got += fpset_resolve_loaded(table, tlog2, f.b | 1ull, idx, v, ctr) ? 1 : 0;
+    } else {
+      got += fpset_insert(table, tlog2, f) == 1;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) got += __shfl_down(got, off);
   if ((threadIdx.x & 63) == 0 && got) atomicAdd(&ctr->next_count, got);
@@ -1335,7 +1341,7 @@ int expand_blocks_per_cu(const Layout& L) {
 hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
                          uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
                          int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags,
-                         uint64_t* sent) {
+                         uint64_t* sent, hipEvent_t mid) {
   if (s_end <= s_begin) return hipSuccess;
   const int cwpb = expand_compact_wpb(L);
   if (cwpb > 0 && !(xflags & XF_LANE_KERNEL) && (box.nshard == 1 || sent)) {
@@ -1391,6 +1397,10 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
       if (e != hipSuccess) return e;
     }
     if (xflags & XF_NO_MATERIALIZE) return hipSuccess;
+    if (mid) {
+      hipError_t e = hipEventRecord(mid, st);
+      if (e != hipSuccess) return e;
+    }
     const size_t mlds = (size_t)cwpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
     RTLA_DISPATCH_N(L, k_materialize, dim3(256 * 16), dim3(64 * cwpb), mlds, st, L, cur, (unsigned long long)cur_base,
                     next, (const unsigned long long*)parents, (unsigned long long)next_base,
@@ -1510,9 +1520,9 @@ hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n
 }
 
 hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed, DevCounters* ctr,
-                              hipStream_t st) {
+                              hipStream_t st, int load_first) {
   hipLaunchKernelGGL(k_probe_bench, dim3(256 * 16), dim3(256), 0, st, (unsigned long long*)table, tlog2,
-                     (unsigned long long)n, (unsigned long long)seed, ctr);
+                     (unsigned long long)n, (unsigned long long)seed, ctr, load_first);
   return hipGetLastError();
 }
 

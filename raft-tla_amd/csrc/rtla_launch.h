@@ -20,7 +20,8 @@ int expand_blocks_per_cu(const Layout& L);
 hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end,
                          uint64_t cur_base, uint32_t* next, uint64_t* parents, uint64_t next_base,
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
-                         int grid, hipStream_t st, int xflags = 0, uint64_t* sent = nullptr);
+                         int grid, hipStream_t st, int xflags = 0, uint64_t* sent = nullptr,
+                         hipEvent_t mid = nullptr);  // recorded between the probe kernel and k_materialize
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
                                 uint64_t max_count, hipStream_t st);
@@ -38,6 +39,6 @@ hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n,
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,
                                uint64_t* info, uint64_t cap, DevCounters* ctr, hipStream_t st);
 hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed,
-                              DevCounters* ctr, hipStream_t st);
+                              DevCounters* ctr, hipStream_t st, int load_first = 0);
 
 }  // namespace rtla

@@ -51,7 +51,7 @@ class _Stats(C.Structure):
                 ("new_states", C.c_uint64), ("generated", C.c_uint64),
                 ("distinct_total", C.c_uint64), ("generated_total", C.c_uint64),
                 ("seconds", C.c_double), ("kernel_ms", C.c_double), ("probes", C.c_uint64),
-                ("row_bytes", C.c_uint64)]
+                ("row_bytes", C.c_uint64), ("expand_ms", C.c_double)]
 
 
 def _load():
@@ -72,6 +72,8 @@ def _load():
         "rtla_coverage": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int]),
         "rtla_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
         "rtla_time_expand": (C.c_int, [C.c_void_p, C.c_int, C.c_int, P(C.c_double)]),
+        "rtla_probe_bench2": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_double), P(C.c_double),
+                                        P(C.c_uint64)]),
         "rtla_row_words": (C.c_int, [P(_Cfg)]),
         "rtla_init_row": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
         "rtla_expand_batch": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, P(C.c_uint32),
@@ -97,7 +99,8 @@ _lib = _load()
 EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset", "rtla_step", "rtla_violation",
             "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
-            "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand"]
+            "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
+            "rtla_probe_bench2"]
 
 
 @dataclass(frozen=True)
@@ -141,6 +144,7 @@ class Level:
     kernel_ms: float = 0.0
     probes: int = 0
     row_bytes: int = 0
+    expand_ms: float = 0.0  # of kernel_ms: the probe kernel alone
 
 
 @dataclass
@@ -278,7 +282,7 @@ class Checker:
 
     def _rec(self, st: _Stats):
         self.levels.append(Level(st.level, st.frontier, st.new_states, st.generated, st.seconds,
-                                 st.kernel_ms, st.probes, st.row_bytes))
+                                 st.kernel_ms, st.probes, st.row_bytes, st.expand_ms))
         self.distinct, self.generated = st.distinct_total, st.generated_total
 
     def init(self) -> int:
@@ -369,6 +373,13 @@ def comm_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(_lib.rtla_comm_id(buf), "rtla_comm_id")
     return buf.raw
+
+
+def probe_bench2(log2: int, n: int):
+    """(s_insert, s_seen_cas, s_seen_load, inserted) for n random keys, see rtla.h."""
+    a, b, c, ins = C.c_double(0), C.c_double(0), C.c_double(0), C.c_uint64(0)
+    _check(_lib.rtla_probe_bench2(log2, n, C.byref(a), C.byref(b), C.byref(c), C.byref(ins)), "rtla_probe_bench2")
+    return a.value, b.value, c.value, ins.value
 
 
 def probe_bench(log2: int, n: int):
