@@ -689,7 +689,7 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 }  // namespace
 
 #ifndef RTLA_COMPACT_WAVES_PER_EU
-#define RTLA_COMPACT_WAVES_PER_EU 1
+#define RTLA_COMPACT_WAVES_PER_EU 3  // 166 VGPRs for N = 3 without spills (the default allocation took 170 -> 2 waves)
 #endif
 template <int NS, bool MULTI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_COMPACT_WAVES_PER_EU)))
