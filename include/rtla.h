@@ -22,6 +22,9 @@
  *   rtla_violation,
  *   rtla_trace               "Error: Invariant X is violated" + "The behavior
  *                            up to this point is:" (TLC's trace file).
+ *   rtla_checkpoint,
+ *   rtla_recover             TLC's -checkpoint / -recover (the `states/` dir,
+ *                            reference .gitignore:2).
  *   rtla_coverage            "-coverage 1" (.vscode/settings.json:5): per-action
  *                            generated / distinct counts.
  *   rtla_expand_batch        TLC's Tool.getNextStates(Next, s) for a batch of
@@ -111,6 +114,13 @@ int rtla_init(rtla_ctx *ctx, rtla_level_stats *out);
 int rtla_reset(rtla_ctx *ctx);
 int rtla_step(rtla_ctx *ctx, rtla_level_stats *out);
 int rtla_violation(rtla_ctx *ctx, int32_t *inv_mask, int32_t *in_model);
+/* TLC's -checkpoint / -recover (reference .gitignore:2, the states/ dir):
+ * write the search (fingerprint set, parent records, current frontier,
+ * counters) between levels to <prefix>.shard<id>.rtla, one file per shard
+ * held by this context; recover it into a context opened with the same
+ * configuration, then continue with rtla_step.  Collective when world > 1. */
+int rtla_checkpoint(rtla_ctx *ctx, const char *prefix);
+int rtla_recover(rtla_ctx *ctx, const char *prefix);
 /* Counterexample, Init first.  rows: n * rtla_row_words() u32; labels: action
  * instance per state (-1 for Init).  *n_rows is set even if cap is too small. */
 int rtla_trace(rtla_ctx *ctx, uint32_t *rows, int32_t *labels, size_t cap, size_t *n_rows);

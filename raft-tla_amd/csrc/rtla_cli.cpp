@@ -186,6 +186,7 @@ void usage() {
   fprintf(stderr,
           "usage: rtla [-workers W] [-coverage M] [-gpus G] [-fpbits B] [-membudget BYTES] [-dump-levels]\n"
           "            [-raft PATH/raft.tla] [-skip-spec-check]\n"
+          "            [-checkpoint MINUTES] [-checkpointdir PREFIX] [-recover PREFIX]\n"
           "            -config FILE.cfg SPEC.tla\n");
 }
 
@@ -221,6 +222,9 @@ int main(int argc, char** argv) {
   bool dump_levels = false, skip_spec_check = false;
   std::string raft_opt;
   uint64_t membudget = 0;
+  // TLC -checkpoint <minutes> / -recover <path> (the reference's .gitignore:2 states/ dir)
+  double ckpt_minutes = 0;
+  std::string ckpt_prefix = "states/ckpt", recover_prefix;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -236,6 +240,9 @@ int main(int argc, char** argv) {
     else if (a == "-dump-levels") dump_levels = true;
     else if (a == "-raft") raft_opt = next();
     else if (a == "-skip-spec-check") skip_spec_check = true;
+    else if (a == "-checkpoint") ckpt_minutes = atof(next().c_str());
+    else if (a == "-checkpointdir") ckpt_prefix = next();
+    else if (a == "-recover") recover_prefix = next();
     else if (a == "-h" || a == "-help") { usage(); return 0; }
     else if (!a.empty() && a[0] == '-') { fprintf(stderr, "Error: unsupported option %s\n", a.c_str()); return 255; }
     else spec = a;
@@ -355,12 +362,28 @@ int main(int argc, char** argv) {
   printf("Computing initial states...\n");
   auto t0 = std::chrono::steady_clock::now();
   rtla_level_stats ls;
-  st = rtla_init(ctx, &ls);
-  printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
-  auto last_progress = t0;
+  memset(&ls, 0, sizeof ls);
+  if (!recover_prefix.empty()) {
+    st = rtla_recover(ctx, recover_prefix.c_str());
+    if (st < 0) { printf("Error: cannot recover from %s: %s\n", recover_prefix.c_str(), rtla_strerror(st)); return 255; }
+    printf("Recovering from checkpoint %s (completed).\n", recover_prefix.c_str());
+  } else {
+    st = rtla_init(ctx, &ls);
+    printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
+  }
+  auto last_progress = t0, last_ckpt = t0;
   while (st == RTLA_OK) {
     st = rtla_step(ctx, &ls);
     if (st < 0) break;
+    if (ckpt_minutes > 0 && st == RTLA_OK &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count() >= ckpt_minutes * 60) {
+      std::string dir = ckpt_prefix.substr(0, ckpt_prefix.rfind('/'));
+      if (ckpt_prefix.find('/') != std::string::npos) (void)!system(("mkdir -p '" + dir + "'").c_str());
+      printf("Checkpointing of run %s\n", ckpt_prefix.c_str());
+      if (rtla_checkpoint(ctx, ckpt_prefix.c_str()) != RTLA_OK) printf("Warning: checkpoint failed\n");
+      else printf("Checkpointing completed at (%s)\n", now_str().c_str());
+      last_ckpt = std::chrono::steady_clock::now();
+    }
     if (dump_levels)
       printf("  level %d: frontier %llu, new %llu, generated %llu, %.3f ms\n", ls.level,
              (unsigned long long)ls.frontier, (unsigned long long)ls.new_states, (unsigned long long)ls.generated,

@@ -499,6 +499,114 @@ static int allreduce_u64(rtla_ctx* x, uint64_t* v, int n, int op) {
   return RTLA_OK;
 }
 
+// ---- checkpoint / recover (TLC's -checkpoint / -recover and its states/
+// directory, reference .gitignore:2).  One file per shard:
+// <prefix>.shard<id>.rtla = header | fingerprint set | sent cache (G > 1) |
+// parent records [0, cur_base + n_cur) | current frontier rows | coverage.
+// Written between levels; a context opened with the same configuration
+// (same cfg, fingerprint-set size and shard count) resumes from it.
+namespace {
+struct CkptHeader {
+  char magic[8];
+  int32_t abi, nshard, shard, W, tlog2, level;
+  rtla_cfg cfg;
+  uint64_t distinct, generated, max_front, cur_base, n_cur, parents_n;
+  int32_t finished, viol_mask, viol_in_model, viol_inst;
+  uint64_t viol_parent, viol_child;
+};
+
+bool write_all(FILE* f, const void* p, size_t n) { return fwrite(p, 1, n, f) == n; }
+bool read_all(FILE* f, void* p, size_t n) { return fread(p, 1, n, f) == n; }
+
+// device <-> file through a bounded host staging buffer
+bool dev_to_file(FILE* f, const void* d, size_t n, std::vector<char>& buf) {
+  for (size_t off = 0; off < n; off += buf.size()) {
+    const size_t m = std::min(buf.size(), n - off);
+    if (hipMemcpy(buf.data(), (const char*)d + off, m, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (!write_all(f, buf.data(), m)) return false;
+  }
+  return true;
+}
+bool file_to_dev(FILE* f, void* d, size_t n, std::vector<char>& buf) {
+  for (size_t off = 0; off < n; off += buf.size()) {
+    const size_t m = std::min(buf.size(), n - off);
+    if (!read_all(f, buf.data(), m)) return false;
+    if (hipMemcpy((char*)d + off, buf.data(), m, hipMemcpyHostToDevice) != hipSuccess) return false;
+  }
+  return true;
+}
+std::string ckpt_path(const char* prefix, int shard) {
+  return std::string(prefix) + ".shard" + std::to_string(shard) + ".rtla";
+}
+}  // namespace
+
+extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
+  if (!x || !prefix) return RTLA_E_ARG;
+  if (!x->inited) return RTLA_E_STATE;
+  HIPCHK(hipSetDevice(x->device));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  std::vector<char> buf(64 << 20);
+  for (auto& s : x->sh) {
+    CkptHeader h;
+    memset(&h, 0, sizeof h);
+    memcpy(h.magic, "RTLACKP1", 8);
+    h.abi = RTLA_ABI_VERSION; h.nshard = x->nshard; h.shard = s.id; h.W = x->L.W; h.tlog2 = x->tlog2;
+    h.level = x->level; h.cfg = x->cfg;
+    h.distinct = x->distinct; h.generated = x->generated; h.max_front = x->max_front;
+    h.cur_base = s.cur_base; h.n_cur = s.n_cur; h.parents_n = s.cur_base + s.n_cur;
+    h.finished = x->finished; h.viol_mask = s.viol_mask; h.viol_in_model = s.viol_in_model;
+    h.viol_inst = s.viol_inst; h.viol_parent = s.viol_parent; h.viol_child = s.viol_child;
+    const std::string path = ckpt_path(prefix, s.id);
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) return RTLA_E_ARG;
+    DevCounters c;
+    bool ok = write_all(f, &h, sizeof h) && dev_to_file(f, s.table, 8ull << x->tlog2, buf) &&
+              (!s.sent || dev_to_file(f, s.sent, 8ull << x->tlog2, buf)) &&
+              dev_to_file(f, s.parents, 8 * h.parents_n, buf) &&
+              dev_to_file(f, s.front[s.cur], 4ull * x->L.W * s.n_cur, buf) &&
+              hipMemcpy(&c, s.ctr, sizeof c, hipMemcpyDeviceToHost) == hipSuccess &&
+              write_all(f, c.cover, sizeof c.cover);
+    ok = fclose(f) == 0 && ok;
+    if (!ok) return RTLA_E_ARG;
+  }
+  return RTLA_OK;
+}
+
+extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
+  if (!x || !prefix) return RTLA_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  std::vector<char> buf(64 << 20);
+  int level = -1;
+  for (auto& s : x->sh) {
+    FILE* f = fopen(ckpt_path(prefix, s.id).c_str(), "rb");
+    if (!f) return RTLA_E_ARG;
+    CkptHeader h;
+    bool ok = read_all(f, &h, sizeof h) && memcmp(h.magic, "RTLACKP1", 8) == 0 && h.abi == RTLA_ABI_VERSION &&
+              h.nshard == x->nshard && h.shard == s.id && h.W == x->L.W && h.tlog2 == x->tlog2 &&
+              memcmp(&h.cfg, &x->cfg, offsetof(rtla_cfg, fpset_log2)) == 0 && h.parents_n <= s.parents_cap &&
+              h.n_cur <= x->front_cap && (level < 0 || level == h.level);
+    DevCounters c;
+    memset(&c, 0, sizeof c);
+    ok = ok && file_to_dev(f, s.table, 8ull << x->tlog2, buf) &&
+         (!s.sent || file_to_dev(f, s.sent, 8ull << x->tlog2, buf)) &&
+         file_to_dev(f, s.parents, 8 * h.parents_n, buf) &&
+         file_to_dev(f, s.front[0], 4ull * x->L.W * h.n_cur, buf) && read_all(f, c.cover, sizeof c.cover);
+    fclose(f);
+    if (!ok) return RTLA_E_STATE;
+    HIPCHK(hipMemcpy(s.ctr, &c, sizeof c, hipMemcpyHostToDevice));
+    level = h.level;
+    s.cur = 0; s.cur_base = h.cur_base; s.n_cur = h.n_cur;
+    s.viol_mask = h.viol_mask; s.viol_in_model = h.viol_in_model; s.viol_inst = h.viol_inst;
+    s.viol_parent = h.viol_parent; s.viol_child = h.viol_child;
+    x->level = h.level; x->distinct = h.distinct; x->generated = h.generated; x->max_front = h.max_front;
+    x->finished = h.finished != 0;
+  }
+  x->init_row.assign(x->L.W, 0);
+  row_init(x->L, x->init_row.data());
+  x->inited = true;
+  return RTLA_OK;
+}
+
 extern "C" int rtla_reset(rtla_ctx* x) {
   if (!x) return RTLA_E_ARG;
   HIPCHK(hipSetDevice(x->device));

@@ -72,6 +72,8 @@ def _load():
         "rtla_coverage": (C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int]),
         "rtla_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
         "rtla_time_expand": (C.c_int, [C.c_void_p, C.c_int, C.c_int, P(C.c_double)]),
+        "rtla_checkpoint": (C.c_int, [C.c_void_p, C.c_char_p]),
+        "rtla_recover": (C.c_int, [C.c_void_p, C.c_char_p]),
         "rtla_probe_bench2": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_double), P(C.c_double),
                                         P(C.c_uint64)]),
         "rtla_row_words": (C.c_int, [P(_Cfg)]),
@@ -100,7 +102,7 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
-            "rtla_probe_bench2"]
+            "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover"]
 
 
 @dataclass(frozen=True)
@@ -255,6 +257,7 @@ class Checker:
         cid = C.create_string_buffer(comm_id, 128) if comm_id else None
         _check(_lib.rtla_open(C.byref(self._cc), rank, world, cid, C.byref(h)), "rtla_open")
         self._h = h
+        self._recovered = False
         self.levels: List[Level] = []
         self.status = OK
 
@@ -303,7 +306,7 @@ class Checker:
         return self.status
 
     def run(self, max_levels: int = 100000) -> int:
-        if not self.levels:
+        if not self.levels and not self._recovered:
             if self.init() != OK:
                 return self.status
         while self.status == OK and len(self.levels) < max_levels:
@@ -339,6 +342,16 @@ class Checker:
         buf = (C.c_uint32 * max(1, n.value * w))()
         _check(_lib.rtla_frontier(self._h, buf, n.value, C.byref(n)), "rtla_frontier")
         return [list(buf[k * w:(k + 1) * w]) for k in range(n.value)]
+
+    def checkpoint(self, prefix: str):
+        """TLC -checkpoint: write the search to <prefix>.shard<id>.rtla (between levels)."""
+        _check(_lib.rtla_checkpoint(self._h, prefix.encode()), "rtla_checkpoint")
+
+    def recover(self, prefix: str):
+        """TLC -recover: resume a checkpoint written by a context of the same configuration."""
+        _check(_lib.rtla_recover(self._h, prefix.encode()), "rtla_recover")
+        self.status = OK
+        self._recovered = True
 
     def time_expand(self, xflags: int, reps: int = 3) -> float:
         """Diagnostic: mean ms of re-expanding the current frontier (pollutes the search)."""
