@@ -548,6 +548,76 @@ static void hash128(const uint8_t *p, size_t n, uint64_t *h1, uint64_t *h2) {
     *h1 = a; *h2 = b | 1;   /* h2 != 0 marks an occupied slot */
 }
 
+/* ----------------------------------------------------------- symmetry -- */
+/* SYMMETRY Permutations(Server) (specs/MC.tla): TLC identifies a state with
+ * its server-permuted images.  The oracle's orbit key is the
+ * lexicographically least serialisation over all N! permutations pi, where
+ * pi relabels every server-valued field (votedFor, the vote sets, the
+ * voterLog and next/matchIndex domains, msource/mdest, eleader, evotes,
+ * evoterLog) and moves server record i to pi(i); bag and elections are
+ * re-sorted.  Any exact orbit invariant gives the same counts. */
+static uint8_t perm_mask(uint8_t m, const int *pi, int N) {
+    uint8_t r = 0;
+    for (int j = 0; j < N; j++) if (m >> j & 1) r |= (uint8_t)(1 << pi[j]);
+    return r;
+}
+static int cmp_msg_cnt(const void *a, const void *b) { return msg_cmp((const Msg *)a, (const Msg *)b); }
+static void permute_state(const orc_cfg *c, const State *s, const int *pi, State *o) {
+    const int N = c->n_server;
+    state_copy(o, s);
+    for (int i = 0; i < N; i++) {
+        const Srv *v = &s->s[i];
+        Srv *w = &o->s[pi[i]];
+        *w = *v;
+        w->voted = v->voted == NIL ? NIL : (uint8_t)pi[v->voted];
+        w->vresp = perm_mask(v->vresp, pi, N); w->vgrant = perm_mask(v->vgrant, pi, N);
+        w->vlp = perm_mask(v->vlp, pi, N);
+        for (int j = 0; j < N; j++) { w->vl[pi[j]] = v->vl[j]; w->next[pi[j]] = v->next[j]; w->match[pi[j]] = v->match[j]; }
+    }
+    /* bag: relabel, then sort (msg, cnt) pairs by message */
+    struct { Msg m; uint8_t cnt; } tmp[KMAX];
+    for (int k = 0; k < s->nmsg; k++) {
+        tmp[k].m = s->msg[k];
+        tmp[k].m.src = (uint8_t)pi[s->msg[k].src]; tmp[k].m.dst = (uint8_t)pi[s->msg[k].dst];
+        tmp[k].cnt = s->cnt[k];
+    }
+    qsort(tmp, (size_t)s->nmsg, sizeof tmp[0], cmp_msg_cnt);
+    for (int k = 0; k < s->nmsg; k++) { o->msg[k] = tmp[k].m; o->cnt[k] = tmp[k].cnt; }
+    for (int k = 0; k < s->nelec; k++) {
+        const Elec *e = &s->elec[k];
+        Elec *f = &o->elec[k];
+        *f = *e;
+        f->leader = (uint8_t)pi[e->leader]; f->votes = perm_mask(e->votes, pi, N); f->vlp = perm_mask(e->vlp, pi, N);
+        for (int j = 0; j < N; j++) f->vl[pi[j]] = e->vl[j];
+    }
+    qsort(o->elec, (size_t)s->nelec, sizeof(Elec), (int (*)(const void *, const void *))elec_cmp);
+}
+/* serialise the orbit representative of s into out; returns its length */
+static size_t serialize_canon(const orc_cfg *c, const State *s, uint8_t *out) {
+    const int N = c->n_server;
+    size_t best = serialize(c, s, out);
+    if (!c->symmetry) return best;
+    int pi[NMAX];
+    for (int i = 0; i < N; i++) pi[i] = i;
+    State *p = (State *)malloc(sizeof(State));
+    uint8_t *tmp = (uint8_t *)malloc(1 << 20);
+    for (;;) {  /* next permutation in lexicographic order */
+        int i = N - 2;
+        while (i >= 0 && pi[i] > pi[i + 1]) i--;
+        if (i < 0) break;
+        int j = N - 1;
+        while (pi[j] < pi[i]) j--;
+        int t = pi[i]; pi[i] = pi[j]; pi[j] = t;
+        for (int a = i + 1, b2 = N - 1; a < b2; a++, b2--) { t = pi[a]; pi[a] = pi[b2]; pi[b2] = t; }
+        permute_state(c, s, pi, p);
+        size_t len = serialize(c, p, tmp);
+        if (len != best) { g_spec_error = 1; break; }  /* impossible: same multiset of values */
+        if (memcmp(tmp, out, len) < 0) memcpy(out, tmp, len);
+    }
+    free(tmp); free(p);
+    return best;
+}
+
 /* ------------------------------------------------------- text printing -- */
 /* Canonical TLC-like value text; identical to oracle/raft_values.py::state_text. */
 typedef struct { char *p; size_t n, cap; } Str;
@@ -780,8 +850,13 @@ static void bfs_emit(void *ud, const State *t, int action, int arg) {
     int isnew = 0;
     size_t len = 0;
     if (inm) {
+        uint64_t h1, h2;
+        if (b->c->symmetry) {  /* orbit key for the seen set; the state itself is explored */
+            len = serialize_canon(b->c, t, e->ser);
+            hash128(e->ser, len, &h1, &h2);
+        }
         len = serialize(b->c, t, e->ser);
-        uint64_t h1, h2; hash128(e->ser, len, &h1, &h2);
+        if (!b->c->symmetry) hash128(e->ser, len, &h1, &h2);
         isnew = seen_put(b->seen, h1, h2);
         if (isnew) {
             arena_push(&b->outs[e->tid], e->ser, len, e->parent_idx, (uint32_t)(action << 16 | arg));
@@ -856,9 +931,10 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
     State *s0 = (State *)malloc(sizeof(State));
     uint8_t *ser = (uint8_t *)malloc(1 << 20);
     init_state(c, s0);
-    size_t len = serialize(c, s0, ser);
+    size_t len = serialize_canon(c, s0, ser);
     uint64_t h1, h2; hash128(ser, len, &h1, &h2);
     seen_put(b.seen, h1, h2);
+    len = serialize(c, s0, ser);
     arena_push(&levels[0], ser, len, UINT64_MAX, 0);
     r->n_levels = 1;
     r->level_new[0] = 1; r->level_gen[0] = 1;

@@ -22,6 +22,8 @@ typedef struct {
     int verbose;
     int max_msgs;           /* 0 = unbounded; else BagCardinality(messages) <= max_msgs */
     uint64_t max_distinct;  /* 0 = unlimited; stop with ORC_E_BUDGET beyond */
+    int symmetry;           /* SYMMETRY Permutations(Server): count server-permutation orbits */
+    int pad_;
 } orc_cfg;
 
 typedef struct {

@@ -19,7 +19,8 @@ MAX_LEVELS = 1024
 class OrcCfg(C.Structure):
     _fields_ = [("n_server", C.c_int), ("n_value", C.c_int), ("max_term", C.c_int),
                 ("max_log", C.c_int), ("max_copies", C.c_int), ("inv_mask", C.c_int),
-                ("verbose", C.c_int), ("max_msgs", C.c_int), ("max_distinct", C.c_uint64)]
+                ("verbose", C.c_int), ("max_msgs", C.c_int), ("max_distinct", C.c_uint64),
+                ("symmetry", C.c_int), ("pad_", C.c_int)]
 
 
 class OrcResult(C.Structure):
@@ -62,11 +63,11 @@ def lib():
 
 
 def cfg_of(n_server, n_value, max_term, max_log, max_copies, max_msgs=0, invariants=(),
-           max_distinct=0):
+           max_distinct=0, symmetry=False):
     m = 0
     for n in invariants:
         m |= INV[n]
-    return OrcCfg(n_server, n_value, max_term, max_log, max_copies, m, 0, max_msgs, max_distinct)
+    return OrcCfg(n_server, n_value, max_term, max_log, max_copies, m, 0, max_msgs, max_distinct, int(symmetry), 0)
 
 
 def bfs(cfg: OrcCfg, threads=8, keep_trace=False, text_hash=False):

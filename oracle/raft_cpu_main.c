@@ -5,7 +5,7 @@
 #include "raft_cpu.h"
 
 int main(int argc, char **argv) {
-    orc_cfg c = {3, 1, 2, 1, 1, 0, 1, 0, 0};
+    orc_cfg c = {3, 1, 2, 1, 1, 0, 1, 0, 0, 0, 0};
     int threads = 8, trace = 0;
     for (int i = 1; i < argc; i++) {
         const char *a = argv[i];
@@ -19,6 +19,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(a, "-i")) { c.inv_mask = atoi(v); i++; }
         else if (!strcmp(a, "-w")) { threads = atoi(v); i++; }
         else if (!strcmp(a, "-m")) { c.max_distinct = strtoull(v, 0, 10); i++; }
+        else if (!strcmp(a, "-s")) { c.symmetry = 1; }
         else if (!strcmp(a, "--trace")) trace = 1;
         else if (!strcmp(a, "-q")) c.verbose = 0;
         else { fprintf(stderr, "unknown arg %s\n", a); return 2; }

@@ -616,6 +616,81 @@ def bfs(cfg: Cfg, max_states: Optional[int] = None) -> BfsResult:
     return BfsResult(levels, len(parent), generated, depth, None, None, max_msgs)
 
 
+# --------------------------------------------------------------- symmetry --
+# SYMMETRY Permutations(Server) (specs/MC.tla).  pi maps server i to pi[i];
+# every server-valued field is relabelled and every function on Server
+# re-indexed.  An independent restatement of oracle/raft_cpu.c's orbit key.
+def permute_state(s: tuple, pi) -> tuple:
+    def srv(x):
+        return x if x == NIL else pi[x]
+
+    def sset(fs):
+        return frozenset(pi[x] for x in fs)
+
+    def on_server(t):  # a function on Server, as a tuple
+        out = [None] * len(t)
+        for i, v in enumerate(t):
+            out[pi[i]] = v
+        return tuple(out)
+
+    def msg(m):
+        d = dict(m.items())
+        d["msource"], d["mdest"] = pi[d["msource"]], pi[d["mdest"]]
+        return FMap(d)
+
+    def elec(e):
+        d = dict(e.items())
+        d["eleader"] = pi[d["eleader"]]
+        d["evotes"] = sset(d["evotes"])
+        d["evoterLog"] = FMap({pi[k]: v for k, v in d["evoterLog"].items()})
+        return FMap(d)
+
+    msgs = FMap({msg(m): c for m, c in s[IX["messages"]].items()})
+    return (
+        msgs,
+        frozenset(elec(e) for e in s[IX["elections"]]),
+        s[IX["allLogs"]],
+        on_server(s[IX["currentTerm"]]),
+        on_server(s[IX["state"]]),
+        on_server(tuple(srv(v) for v in s[IX["votedFor"]])),
+        on_server(s[IX["log"]]),
+        on_server(s[IX["commitIndex"]]),
+        on_server(tuple(sset(v) for v in s[IX["votesResponded"]])),
+        on_server(tuple(sset(v) for v in s[IX["votesGranted"]])),
+        on_server(tuple(FMap({pi[k]: v for k, v in f.items()}) for f in s[IX["voterLog"]])),
+        on_server(tuple(on_server(row) for row in s[IX["nextIndex"]])),
+        on_server(tuple(on_server(row) for row in s[IX["matchIndex"]])),
+    )
+
+
+def orbit_key(cfg: Cfg, s: tuple) -> str:
+    """The least canonical text over all server permutations of s."""
+    import itertools
+    return min(state_text(cfg, permute_state(s, pi)) for pi in itertools.permutations(range(cfg.n_server)))
+
+
+def bfs_symmetric(cfg: Cfg) -> List[Tuple[int, int]]:
+    """Per-level (new orbits, generated) of the BFS under SYMMETRY
+    Permutations(Server): a successor is new iff no state of its orbit was
+    seen; the state itself (not a representative) is explored, as in TLC."""
+    s0 = init_state(cfg)
+    seen = {orbit_key(cfg, s0)}
+    levels, frontier = [(1, 1)], [s0]
+    while frontier:
+        nxt, gen = [], 0
+        for s in frontier:
+            for _lab, t in next_states(cfg, s):
+                gen += 1
+                if in_model(cfg, t):
+                    k = orbit_key(cfg, t)
+                    if k not in seen:
+                        seen.add(k)
+                        nxt.append(t)
+        levels.append((len(nxt), gen))
+        frontier = nxt
+    return levels
+
+
 # ------------------------------------------------------------ state text --
 # Canonical TLC-like text; must be byte-identical to oracle/raft_cpu.c's
 # state_text (sets and the bag's domain sorted by their text).

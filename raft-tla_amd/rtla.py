@@ -122,6 +122,7 @@ class Config:
     mem_budget: int = 0
     shards: int = 0
     chunk: int = 0
+    symmetry: bool = False  # SYMMETRY Permutations(Server) (specs/MC.tla)
 
     @property
     def inv_mask(self) -> int:
@@ -132,7 +133,7 @@ class Config:
 
     def c(self) -> _Cfg:
         return _Cfg(self.n_server, self.n_value, self.max_term, self.max_log, self.max_copies,
-                    self.max_msgs, self.bag_cap, self.elec_cap, self.inv_mask, 0,
+                    self.max_msgs, self.bag_cap, self.elec_cap, self.inv_mask, int(self.symmetry),
                     self.fpset_log2, self.shards, self.frontier_cap, self.mem_budget, self.chunk)
 
 

@@ -32,6 +32,16 @@ CASES = {
     "n3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, (NTL,), False, True),
     "n3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, (ES, LM), False, True),
 }
+# SYMMETRY Permutations(Server) (specs/MC.tla): per-level orbit counts.  "py"
+# cases are also run through the value oracle's independent orbit BFS.
+# name: (N, V, T, L, C, M, invariants, py, big)
+SYM_CASES = {
+    "n2_v1_t2_l1_m1_sym": (2, 1, 2, 1, 1, 1, (NTL,), True, False),
+    "n2_v1_t3_l1_m1_sym": (2, 1, 3, 1, 1, 1, (NTL, ES, LM), True, False),
+    "n3_v1_t2_l1_m1_sym": (3, 1, 2, 1, 1, 1, (NTL,), False, False),
+    "n3_v1_t3_l1_m1_ntl_sym": (3, 1, 3, 1, 1, 1, (NTL,), False, False),
+    "n3_v1_t2_l1_m2_sym": (3, 1, 2, 1, 1, 2, (NTL,), False, True),
+}
 # Models too large for the CPU oracle to exhaust here: a bounded prefix of
 # complete BFS levels (the oracle stops after the first level that passes
 # max_distinct).  name: (N, V, T, L, C, M, invariants, max_distinct)
@@ -66,6 +76,22 @@ def main():
                 ph = rv.level_text_hashes(pc)
                 assert ph == r["level_text_hash"][:len(ph)], name
             case["source"] += " + oracle/raft_values.py"
+        out[name] = case
+        print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
+    for name, (n, v, t, l, c, m, inv, py, is_big) in SYM_CASES.items():
+        if is_big and not big:
+            continue
+        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, symmetry=True)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big)
+        assert r["rc"] >= 0, (name, r["rc"])
+        case = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
+                "invariants": list(inv), "symmetry": True, "distinct": r["distinct"], "generated": r["generated"],
+                "depth": r["depth"], "levels": r["levels"], "violated": r["violated"], "trace_len": r["trace_len"],
+                "source": "oracle/raft_cpu.c (orbit key: least serialisation over server permutations)"}
+        if py and not r["violated"]:
+            pl = rv.bfs_symmetric(rv.Cfg(n, v, t, l, c, inv, m))
+            assert [list(x) for x in pl] == r["levels"], name
+            case["source"] += " + oracle/raft_values.py (orbit key: least text over permutations)"
         out[name] = case
         print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
     for name, (n, v, t, l, c, m, inv, cap) in PREFIXES.items():

@@ -27,6 +27,7 @@ HASHED = sorted(k for k, v in GOLD.items() if "level_text_hash" in v)
 
 
 def cfg_of(g, **kw):
+    kw.setdefault("symmetry", bool(g.get("symmetry", False)))
     return rtla.Config(g["n_server"], g["n_value"], g["max_term"], g["max_log"], g["max_copies"],
                        g["max_msgs"], tuple(g["invariants"]), **kw)
 
