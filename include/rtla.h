@@ -76,7 +76,7 @@ typedef struct {
     int32_t bag_cap;     /* distinct messages per row; 0 = auto (max_msgs + 1, or 32) */
     int32_t elec_cap;    /* election records per row; 0 = auto ((max_term - 1) * n_server) */
     int32_t inv_mask;    /* RTLA_INV_* */
-    int32_t symmetry;    /* must be 0 in this version */
+    int32_t symmetry;    /* 1: SYMMETRY Permutations(Server) (specs/MC.tla Perms): orbit counts */
     int32_t fpset_log2;  /* log2(#8-byte slots) of this rank's fingerprint set; 0 = auto */
     int32_t shards;      /* world == 1 only: split the search on this GPU into this many
                             fingerprint-owned shards (same exchange protocol as multi-GPU,

@@ -95,6 +95,7 @@ std::string now_str() {
 // ------------------------------------------------------------ cfg parse ----
 struct CfgFile {
   std::string specification;
+  std::string symmetry;  // SYMMETRY operator name ("" = none)
   std::vector<std::string> invariants, constraints;
   std::map<std::string, std::vector<std::string>> sets;  // Name = {a, b}
   std::map<std::string, std::string> scalars;            // Name = "x" | 3 | mv
@@ -170,7 +171,8 @@ bool parse_cfg(const std::string& text, CfgFile* c, std::string* err) {
       }
       continue;
     }
-    if (mode == "SYMMETRY" || mode == "VIEW" || mode == "PROPERTY" || mode == "PROPERTIES" || mode == "INIT" ||
+    if (mode == "SYMMETRY") { c->symmetry = t[i++]; continue; }
+    if (mode == "VIEW" || mode == "PROPERTY" || mode == "PROPERTIES" || mode == "INIT" ||
         mode == "NEXT" || mode == "ACTION_CONSTRAINT" || mode == "ACTION_CONSTRAINTS") {
       *err = mode + " is not supported by this checker";
       return false;
@@ -310,6 +312,14 @@ int main(int argc, char** argv) {
              k.c_str());
       return 150;
     }
+  }
+  if (!cf.symmetry.empty()) {
+    if (!wrapper || cf.symmetry != "Perms") {
+      printf("Error: The symmetry %s specified in the configuration file is not defined in the specification.\n",
+             cf.symmetry.c_str());
+      return 150;
+    }
+    c.symmetry = 1;  // Perms == Permutations(Server) (specs/MC.tla)
   }
   if (cf.constraints.empty()) {
     printf("Error: no CONSTRAINT: raft.tla's state space is infinite (Timeout raft.tla:180 and Send raft.tla:106-110 "

@@ -130,13 +130,13 @@ struct rtla_ctx {
 
 static int layout_from_cfg(const rtla_cfg* c, Layout* L) {
   if (!c) return RTLA_E_ARG;
-  if (c->symmetry) return RTLA_E_CONFIG;
   int K = c->bag_cap ? c->bag_cap : (c->max_msgs > 0 ? c->max_msgs + 1 : 32);
   int E = c->elec_cap ? c->elec_cap : (c->max_term - 1) * c->n_server;
   if (E < 1) E = 1;
   if (make_layout(L, c->n_server, c->n_value, c->max_term, c->max_log, c->max_copies, c->max_msgs, K, E,
                   c->inv_mask) != 0)
     return RTLA_E_CONFIG;
+  L->sym = c->symmetry ? 1 : 0;
   return RTLA_OK;
 }
 
@@ -465,7 +465,7 @@ static int env_xflags() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RTLA_XFLAGS");
-    v = e ? (atoi(e) & (XF_LANE_KERNEL | XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY)) : 0;
+    v = e ? (atoi(e) & (XF_LANE_KERNEL | XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL)) : 0;
   }
   return v;
 }

@@ -29,6 +29,7 @@ using namespace rtla;
 namespace {
 
 constexpr int STAGE_ROWS = 16;  // LDS staging rows per wave
+constexpr int PERM_MAX = 120;   // NMAX! server permutations (symmetry)
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -171,7 +172,7 @@ __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
 // words so every wave's hash slots stay 8-byte aligned.
 __host__ __device__ constexpr int even_words(int W) { return (W + 1) & ~1; }
 __host__ __device__ constexpr int wave_lds_words(int W) {
-  return (even_words(W) + 32 + 4 * NMAX + STAGE_ROWS * W + 3) & ~3;
+  return (even_words(W) + 32 + 4 * NMAX + STAGE_ROWS * W + 4 * PERM_MAX + 3) & ~3;
 }
 
 // (the readlane builtins return a signed int: widen through uint32_t)
@@ -220,14 +221,27 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
   uint32_t* pall = prow + even_words(W);
   FP* hsrv = reinterpret_cast<FP*>(pall + 32);
   uint32_t* stage = pall + 32 + 4 * NMAX;
+  FP* permfp = reinterpret_cast<FP*>(stage + STAGE_ROWS * W);  // [PERM_MAX]: fp(pi(parent)) + allLogs'
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
 
   unsigned long long my_gen = 0, my_probe = 0;
   const int fixed = L.fam[F_RECEIVE];
+  int nperm = 1;
+#pragma unroll
+  for (int i = 2; i <= NS; i++) nperm *= i;
   for (unsigned long long s = s_begin + (unsigned long long)blockIdx.x * wpb + wave; s < s_end;
        s += (unsigned long long)gridDim.x * wpb) {
     const FP pfp = load_parent<NS>(L, cur + s * (unsigned long long)W, prow, pall, hsrv, lane);
+    if (L.sym) {  // SYMMETRY: per-permutation fingerprints of the parent, lanes over permutations
+      const FP afp = alllogs_fp(L, pall);  // allLogs' is the same for every successor (raft.tla:465)
+      for (int k = lane; k < nperm; k += 64) {
+        int pi[NS], inv[NS];
+        kth_perm<NS>(k, pi, inv);
+        permfp[k] = fp_add(perm_row_fp<NS>(L, prow, pi, inv), afp);
+      }
+      wave_sync();
+    }
     const int nmsg = row_nmsg(L, prow);
     const int ncand = fixed + 3 * nmsg;
     for (int base = 0; base < ncand; base += 64) {
@@ -249,10 +263,23 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
       FP cfp{0, 0};
       if (en && d.in_model) {
         cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, d.srv >= 0 ? &hsrv[d.srv] : nullptr));
-        const int owner = fp_owner(cfp, box.nshard);
+        // seen-set key: the state's own fingerprint, or under SYMMETRY its
+        // orbit key (least fingerprint over the server permutations)
+        FP key = cfp;
+        if (L.sym) {
+          key = FP{~0ull, ~0ull};
+          for (int k = 0; k < nperm; k++) {
+            int pi[NS], inv[NS];
+            kth_perm<NS>(k, pi, inv);
+            const FP f = fp_add(permfp[k], perm_delta_fp<NS>(L, prow, d, pi, inv));
+            if (fp_less(f, key)) key = f;
+          }
+          key = orbit_key_finish(key);
+        }
+        const int owner = fp_owner(key, box.nshard);
         if (owner == box.me) {
           my_probe++;
-          int r = fpset_insert(table, tlog2, cfp);
+          int r = fpset_insert(table, tlog2, key);
           if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
           isnew = r == 1;
         } else {
@@ -261,8 +288,8 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
           unsigned long long slot = atomicAdd(&box.out_count[owner], 1ull);
           if (slot < box.cap) {
             unsigned long long k = (unsigned long long)owner * box.cap + slot;
-            box.send_fp[2 * k] = cfp.a;
-            box.send_fp[2 * k + 1] = cfp.b;
+            box.send_fp[2 * k] = key.a;
+            box.send_fp[2 * k + 1] = key.b;
             box.send_ref[k] = s << 16 | (unsigned long long)inst;
           } else {
             set_flag(ctr, FLAG_OUTBOX_FULL);
@@ -775,7 +802,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
             const unsigned long long k = (unsigned long long)o * box.cap + slot;
             box.send_fp[2 * k] = pf.a;
             box.send_fp[2 * k + 1] = pf.b;
-            box.send_ref[k] = ((prec >> 16) & ((1ull << 40) - 1ull)) - cur_base << 16 | (prec & 0xffffull);
+            box.send_ref[k] = (((prec >> 16) & ((1ull << 40) - 1ull)) - cur_base) << 16 | (prec & 0xffffull);
           } else {
             set_flag(ctr, FLAG_OUTBOX_FULL);
           }
@@ -1344,7 +1371,7 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
                          uint64_t* sent, hipEvent_t mid) {
   if (s_end <= s_begin) return hipSuccess;
   const int cwpb = expand_compact_wpb(L);
-  if (cwpb > 0 && !(xflags & XF_LANE_KERNEL) && (box.nshard == 1 || sent)) {
+  if (cwpb > 0 && !L.sym && !(xflags & (XF_LANE_KERNEL | XF_WAVE_KERNEL)) && (box.nshard == 1 || sent)) {
     const bool multi = box.nshard > 1;
     {  // k_materialize's range starts at the next-frontier count before this launch
       hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
@@ -1408,7 +1435,7 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
     return hipGetLastError();
   }
   const int wpb = expand_lane_wpb(L);
-  if (wpb > 0) {  // one lane per state (rows fit LDS)
+  if (wpb > 0 && !L.sym && !(xflags & XF_WAVE_KERNEL)) {  // one lane per state (rows fit LDS)
     {  // k_materialize's range starts at the next-frontier count before this launch
       hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
                                     hipMemcpyDeviceToDevice, st);
@@ -1445,7 +1472,8 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
                     (unsigned long long)next_cap, ctr);
     return hipGetLastError();
   }
-  // rows too wide for 64 per wave in LDS: one wave per state
+  // one wave per state: rows too wide for 64 per wave in LDS, or SYMMETRY
+  // (the orbit key needs the full Delta of each successor)
   RTLA_DISPATCH_N(L, k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
                   (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base, next,
                   (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,

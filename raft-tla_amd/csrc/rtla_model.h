@@ -86,6 +86,7 @@ enum { INV_NO_TWO_LEADERS = 1, INV_ELECTION_SAFETY = 2, INV_LOG_MATCHING = 4 };
 struct Layout {
   int N, V, T, L, C, M, K, E;
   int inv_mask;
+  int sym;             // SYMMETRY Permutations(Server): dedup by orbit key (orbit_key)
   int SW, EW;
   int off_hdr, off_srv, off_all, all_words, off_elec, off_bag, W;
   int n_logs;          // |{logs of length <= L, terms 1..T}|
@@ -102,6 +103,7 @@ static inline int make_layout(Layout* l, int N, int V, int T, int L, int C, int 
   if (M > 0 && K < M + 1) return -1;  // out-of-model successors must stay representable
   l->N = N; l->V = V; l->T = T; l->L = L; l->C = C; l->M = M; l->K = K; l->E = E;
   l->inv_mask = inv_mask;
+  l->sym = 0;
   l->SW = 3 + N;
   l->EW = 2 + N;
   int B = T * V, off = 0, pw = 1;
@@ -842,6 +844,214 @@ RTLA_HD void materialize(const Layout& L, P row, const Delta& d, R all_new, FP f
       child[L.off_bag + 2 * d.op_slot[q] + 1] = (uint32_t)(d.op_new[q] >> 32);
     }
   }
+}
+
+// ------------------------------------------------------------ symmetry ----
+// SYMMETRY Permutations(Server) (specs/MC.tla).  TLC identifies a state with
+// its server-permuted images.  The dedup key of a successor is the least
+// (a, b) over all N! permutations pi of the fingerprint of pi(state): record
+// i moves to position pi[i] and every server-valued field is relabelled
+// (votedFor, votesResponded/Granted, voterLog and next/matchIndex domains,
+// msource/mdest, eleader, evotes, evoterLog).  The fingerprint being a sum
+// of per-component hashes, fp(pi(child)) = fp(pi(parent)) + the relabelled
+// hashes of the few components the action changes: the kernel computes the
+// N! parent values once per frontier state and then pays, per successor and
+// permutation, two server-record hashes, two per bag-slot write and one per
+// new election record.  The row keeps the state itself (and its own
+// fingerprint): TLC explores the state it generated, and the orbit key is
+// used only for the seen set and shard ownership.
+
+// k-th permutation of 0..N-1 in lexicographic order (Lehmer code)
+template <int NS>
+RTLA_HD void kth_perm(int k, int* pi, int* inv) {
+  int avail = (1 << NS) - 1;
+  int f = 1;
+#pragma unroll
+  for (int i = 2; i < NS; i++) f *= i;  // (NS-1)!
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
+    const int idx = f ? k / f : 0;
+    k -= idx * f;
+    int pick = 0, seen = -1;
+#pragma unroll
+    for (int b = 0; b < NS; b++)
+      if (avail >> b & 1) {
+        seen++;
+        if (seen == idx) pick = b;
+      }
+    pi[i] = pick;
+    avail &= ~(1 << pick);
+    if (NS - 1 - i > 0) f /= (NS - 1 - i);
+  }
+#pragma unroll
+  for (int i = 0; i < NS; i++)
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+      if (pi[j] == i) inv[i] = j;
+}
+template <int NS>
+RTLA_HD uint32_t perm_mask(uint32_t m, const int* pi) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < NS; j++) r |= ((m >> j) & 1u) << pi[j];
+  return r;
+}
+template <int NS>
+RTLA_HD uint32_t sel_word(const uint32_t* a, int i) {  // a[i] for a run-time i, as selects
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < NS; k++)
+    if (k == i) r = a[k];
+  return r;
+}
+// server record relabelled by pi (the record of server i, now at pi[i])
+template <int NS>
+RTLA_HD void perm_srv_rec(const uint32_t* rec, const int* pi, const int* inv, uint32_t* out) {
+  const uint32_t w0 = rec[0], vf = s_voted(w0);
+  uint32_t vfp = vf;
+#pragma unroll
+  for (int j = 0; j < NS; j++)
+    if (vf == (uint32_t)j) vfp = (uint32_t)pi[j];
+  out[0] = s_make(s_term(w0), s_role(w0), vfp, s_commit(w0), perm_mask<NS>(s_vresp(w0), pi),
+                  perm_mask<NS>(s_vgrant(w0), pi), perm_mask<NS>(s_vlp(w0), pi));
+  out[1] = rec[1];
+  uint32_t nm = 0;
+  uint32_t vl[NS];
+#pragma unroll
+  for (int j = 0; j < NS; j++) vl[j] = rec[3 + j];
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    const int j = inv[k];  // field k of the image = field inv[k] of the original
+    nm |= nm_next(rec[2], j) << (3 * k) | nm_match(rec[2], j) << (15 + 3 * k);
+    out[3 + k] = sel_word<NS>(vl, j);
+  }
+  out[2] = nm;
+}
+template <int NS>
+RTLA_HD uint64_t perm_msg_slot(uint64_t v, const int* pi) {  // msource bits 2-4, mdest bits 5-7
+  if (!v) return 0;  // empty slot (h_msg(0) = 0)
+  const uint32_t src = m_src(v), dst = m_dst(v);
+  uint32_t ps = src, pd = dst;
+#pragma unroll
+  for (int j = 0; j < NS; j++) {
+    if (src == (uint32_t)j) ps = (uint32_t)pi[j];
+    if (dst == (uint32_t)j) pd = (uint32_t)pi[j];
+  }
+  return (v & ~(63ull << 2)) | (uint64_t)ps << 2 | (uint64_t)pd << 5;
+}
+template <int NS>
+RTLA_HD void perm_elec(const uint32_t* e, const int* pi, const int* inv, uint32_t* out) {
+  const uint32_t w0 = e[0], ld = (w0 >> 4) & 7u;
+  uint32_t pl = ld;
+#pragma unroll
+  for (int j = 0; j < NS; j++)
+    if (ld == (uint32_t)j) pl = (uint32_t)pi[j];
+  out[0] = (w0 & 15u) | pl << 4 | perm_mask<NS>((w0 >> 7) & 31u, pi) << 7 | perm_mask<NS>((w0 >> 12) & 31u, pi) << 12;
+  out[1] = e[1];
+  uint32_t vl[NS];
+#pragma unroll
+  for (int j = 0; j < NS; j++) vl[j] = e[2 + j];
+#pragma unroll
+  for (int k = 0; k < NS; k++) out[2 + k] = sel_word<NS>(vl, inv[k]);
+}
+
+// Fingerprint of pi(row) without its allLogs part (permutation-free):
+// N server records, the bag and the election records, relabelled.
+template <int NS, class P>
+RTLA_HD FP perm_row_fp(const Layout& L, P row, const int* pi, const int* inv) {
+  constexpr int SW = 3 + NS, EW = 2 + NS;
+  FP f{0, 0};
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
+    uint32_t rec[SW], out[SW];
+    load_rec<NS>(L, row, i, rec);
+    perm_srv_rec<NS>(rec, pi, inv, out);
+    f = fp_add(f, h_srv(pi[i], out, SW));
+  }
+  const int nm = row_nmsg(L, row), ne = row_nelec(L, row);
+  for (int q = 0; q < nm; q++) f = fp_add(f, h_msg(perm_msg_slot<NS>(bag_slot(L, row, q), pi)));
+  for (int e = 0; e < ne; e++) {
+    uint32_t er[EW], out[EW];
+#pragma unroll
+    for (int w = 0; w < EW; w++) er[w] = row[L.off_elec + e * EW + w];
+    perm_elec<NS>(er, pi, inv, out);
+    f = fp_add(f, h_elec(out, EW));
+  }
+  return f;
+}
+
+// fp(pi(row + d)) - fp(pi(row)): only the components the delta changes
+// (one server record, <= 3 bag slots, one appended election record).
+template <int NS, class P>
+RTLA_HD FP perm_delta_fp(const Layout& L, P row, const Delta& d, const int* pi, const int* inv) {
+  constexpr int SW = 3 + NS, EW = 2 + NS;
+  FP f{0, 0};
+  if (d.srv >= 0) {
+    uint32_t rec[SW], out[SW];
+    load_rec<NS>(L, row, d.srv, rec);
+    int to = 0;
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+      if (j == d.srv) to = pi[j];
+    perm_srv_rec<NS>(rec, pi, inv, out);
+    f = fp_sub(f, h_srv(to, out, SW));
+    perm_srv_rec<NS>(d.rec, pi, inv, out);
+    f = fp_add(f, h_srv(to, out, SW));
+  }
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+    if (q < d.nops)
+      f = fp_add(f, fp_sub(h_msg(perm_msg_slot<NS>(d.op_new[q], pi)), h_msg(perm_msg_slot<NS>(d.op_old[q], pi))));
+  if (d.elec) {
+    uint32_t out[EW];
+    perm_elec<NS>(d.erec, pi, inv, out);
+    f = fp_add(f, h_elec(out, EW));
+  }
+  return f;
+}
+
+RTLA_HD bool fp_less(FP x, FP y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }
+
+// The least of N! fingerprints is skewed towards 0 (density N!(1-x)^(N!-1)),
+// which would pile the orbit keys into the low slots of the open-addressing
+// set.  Re-mix it with a bijection of the 128 bits (mix_b and mix_a are
+// bijective; a' depends on b only through an xor) so home slots and shard
+// ownership are uniform again and no two orbit keys merge.
+RTLA_HD FP orbit_key_finish(FP m) {
+  return FP{mix_a(m.a ^ (m.b >> 29 | m.b << 35)), mix_b(m.b)};
+}
+
+// Orbit key of a row from scratch: least fingerprint over all N! server
+// permutations (host: Init and tests; the kernels derive it per successor
+// from per-permutation parent fingerprints, k_expand).
+template <int NS, class P>
+RTLA_HD FP orbit_key(const Layout& L, P row, FP all_fp) {
+  int nperm = 1;
+#pragma unroll
+  for (int i = 2; i <= NS; i++) nperm *= i;
+  FP best{~0ull, ~0ull};
+  for (int k = 0; k < nperm; k++) {
+    int pi[NS], inv[NS];
+    kth_perm<NS>(k, pi, inv);
+    const FP f = fp_add(perm_row_fp<NS>(L, row, pi, inv), all_fp);
+    if (fp_less(f, best)) best = f;
+  }
+  return orbit_key_finish(best);
+}
+
+// allLogs part of a fingerprint: sum of h_all over the set bits of the words
+template <class Q>
+RTLA_HD FP alllogs_fp(const Layout& L, Q words) {
+  FP f{0, 0};
+  for (int w = 0; w < L.all_words; w++) {
+    uint32_t m = words[w];
+    while (m) {
+      const int b = __builtin_ctz(m);
+      m &= m - 1;
+      f = fp_add(f, h_all(w * 32 + b));
+    }
+  }
+  return f;
 }
 
 // ---------------------------------------------------------- invariants ----

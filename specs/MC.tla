@@ -8,7 +8,7 @@
 \* build's own definitions; every state count this repository reports is
 \* relative to them.  The MI355X checker (raft-tla_amd/) and both oracles
 \* (oracle/raft_values.py, oracle/raft_cpu.c) implement exactly these.
-EXTENDS raft
+EXTENDS raft, TLC
 
 CONSTANTS MaxTerm,      \* currentTerm bound
           MaxLogLen,    \* Len(log) bound
@@ -32,6 +32,11 @@ NoTwoLeaders == \A i, j \in Server :
 
 \* History-variable form of Election Safety (raft.tla:34-39 `elections`).
 ElectionSafety == \A e, f \in elections : e.eterm = f.eterm => e.eleader = f.eleader
+
+\* Server symmetry (cfg: SYMMETRY Perms).  Every action of raft.tla treats
+\* servers alike, so TLC may identify states that differ by a renaming of
+\* Server: distinct-state counts become orbit counts.
+Perms == Permutations(Server)
 
 LogMatching == \A i, j \in Server :
                  \A n \in 1..(IF Len(log[i]) < Len(log[j]) THEN Len(log[i]) ELSE Len(log[j])) :

@@ -335,3 +335,78 @@ def test_recover_rejects_other_configuration(tmp_path):
     with rtla.Checker(cfg_of(other, **kw)) as b:
         with pytest.raises(rtla.RtlaError):
             b.recover(prefix)
+
+
+# ---- SYMMETRY Permutations(Server) (specs/MC.tla Perms) ----
+# The golden orbit counts come from the C oracle (least serialisation over
+# server permutations) and, for N=2, the value oracle's orbit BFS; the GPU
+# keys the seen set by the least FINGERPRINT over permutations instead, so
+# agreement checks the orbit relation, not a shared implementation.
+SYM_SMALL = sorted(k for k in SMALL if GOLD[k].get("symmetry"))
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("name", SYM_SMALL)
+def test_symmetry_virtual_shards_match_golden(name, shards):
+    """Orbit-key ownership: the exchange protocol must find each orbit once."""
+    g = GOLD[name]
+    kw = small_kw(g)
+    kw["mem_budget"] *= shards
+    res = rtla.check(cfg_of(g, shards=shards, chunk=700, **kw), trace=False)
+    assert [[lv.new, lv.generated] for lv in res.levels] == g["levels"]
+    assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_symmetry_counterexample_trace(shards):
+    """Same shortest depth as without symmetry; the trace is made of the
+    states actually generated, so it replays step by step in the oracle."""
+    g = GOLD["n3_v1_t3_l1_m1_ntl_sym"]
+    kw = small_kw(g)
+    kw["mem_budget"] *= shards
+    res = rtla.check(cfg_of(g, shards=shards, **kw))
+    assert res.violation == "NoTwoLeaders"
+    assert len(res.trace) == g["depth"] == GOLD["n3_v1_t3_l1_m1_ntl"]["depth"]
+    walk = raft_cpu.Walk(raft_cpu.cfg_of(3, 1, 3, 1, 1, 1, ("NoTwoLeaders",)))
+    assert walk.text() == res.trace[0][1]
+    for label, text in res.trace[1:]:
+        assert text in [t for _, t in walk.successors()], label
+        walk.goto(text)
+    assert walk.invariants() & 1
+
+
+def test_symmetry_stored_rows_are_generated_states():
+    """Rows keep the state that was generated (not a canonical image) with
+    its own fingerprint; each level holds one state per new orbit."""
+    g = GOLD["n3_v1_t2_l1_m1_sym"]
+    cfg = cfg_of(g, **small_kw(g))
+    with rtla.Checker(cfg) as ck:
+        st = ck.init()
+        level = 1
+        while st == rtla.OK and level < 14:
+            st = ck.step()
+            level += 1
+            rows = ck.frontier()
+            assert len(rows) == g["levels"][level - 1][0]
+            assert all(rtla.stored_fingerprint(r) == rtla.row_fingerprint(cfg, r) for r in rows)
+            assert len({rtla.state_text(cfg, r) for r in rows}) == len(rows)
+
+
+def test_wave_kernel_without_symmetry_matches_golden():
+    """The wave-per-state k_expand (the symmetry path) on plain models, forced
+    with RTLA_XFLAGS=2048 in a child process (the flag is read once)."""
+    import subprocess
+    import sys
+    code = ("import json, rtla, sys; g = json.load(open(sys.argv[1]))['n2_v2_t3_l2_m1'];"
+            "r = rtla.check(rtla.Config(g['n_server'], g['n_value'], g['max_term'], g['max_log'], g['max_copies'],"
+            " g['max_msgs'], tuple(g['invariants']), fpset_log2=20, mem_budget=1 << 30), trace=False);"
+            "assert [[lv.new, lv.generated] for lv in r.levels] == g['levels'], 'levels differ';"
+            "assert (r.distinct, r.generated, r.depth) == (g['distinct'], g['generated'], g['depth']);"
+            "print('ok', r.distinct)")
+    env = dict(os.environ, RTLA_XFLAGS="2048",
+               PYTHONPATH=os.pathsep.join([os.path.join(os.path.dirname(__file__), "..", "raft-tla_amd"),
+                                           os.environ.get("PYTHONPATH", "")]))
+    out = subprocess.run([sys.executable, "-c", code, os.path.join(os.path.dirname(__file__), "golden",
+                                                                   "bfs_counts.json")],
+                         env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
