@@ -37,7 +37,7 @@ WORKLOADS = {
 }
 DEFAULT = "raft3_v2_t2_l2_m2"
 # fingerprint-set size per workload (distinct states: 2.41e9, 2.54e9, 1.45e8)
-FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 32, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30}
+FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30}
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Random 8-byte fingerprint-set accesses into a 32 GiB table (far beyond the
 # 256 MiB Infinity Cache), all CUs, measured on MI355X by tools/probe_calib.py
@@ -95,8 +95,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fpset-log2", type=int, default=0,
                     help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the "
-                         "workload (2^32 slots = 32 GiB for the 2.4e9-state default at 56%% load, fewer per "
-                         "rank when sharded)")
+                         "workload (2^33 slots = 64 GiB for the 2.4e9-state default at 28%% load: 11%% faster "
+                         "than 2^32 at 56%%, fewer long probe chains per wave, tools/fpset_sweep.sh; 2^34 leaves "
+                         "too little HBM for the frontiers; fewer per rank when sharded)")
     ap.add_argument("--levels", action="store_true", help="print the per-level table to stderr")
     ap.add_argument("--shards", type=int, default=0,
                     help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
