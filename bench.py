@@ -66,6 +66,36 @@ def load_traffic(workload, launches):
     return best
 
 
+def fpset_log2_for(workload, world, override=0):
+    """log2 fingerprint-set slots per rank: the workload's single-GPU size,
+    divided by the next power of two >= world (each rank owns 1/world of the
+    fingerprints, so the load stays ~28 %); an explicit override is per rank."""
+    fpl = override or FPSET_LOG2.get(workload, 30)
+    if not override and world > 1:
+        fpl = max(24, fpl - (world - 1).bit_length())
+    return fpl
+
+
+def share_comm_id(rank, make_id):
+    """Rank 0 creates the RCCL unique id, every rank receives it (gloo is the
+    control plane only; the data path is the library's own communicator)."""
+    import torch.distributed as dist
+    box = [make_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def max_over_ranks(x, world):
+    """The job's time is the slowest rank's."""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    tt = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
 def dist_env():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
         int(os.environ.get("LOCAL_RANK", "0"))
@@ -112,15 +142,11 @@ def main():
         # gloo = control plane only (RCCL id broadcast, barriers, max-reduce of
         # times); the data path is the library's own RCCL communicator.
         dist.init_process_group("gloo")
-        box = [rtla.comm_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        comm_id = box[0]
+        comm_id = share_comm_id(rank, rtla.comm_id)
 
     shape = WORKLOADS[args.workload]
     n, v, t, l, c, m, inv = shape
-    fpl = args.fpset_log2 or FPSET_LOG2.get(args.workload, 30)
-    if not args.fpset_log2 and world > 1:  # each rank owns 1/world of the fingerprints
-        fpl = max(24, fpl - (world - 1).bit_length())
+    fpl = fpset_log2_for(args.workload, world, args.fpset_log2)
     cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=fpl, shards=args.shards,
                       mem_budget=(200 << 30) if args.shards > 1 else 0)
     ck = rtla.Checker(cfg, rank=rank, world=world, comm_id=comm_id)
@@ -146,13 +172,7 @@ def main():
         runs.append(one_run())
     t1 = time.perf_counter()
     barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(t1 - t0, world)
 
     levels = runs[-1]
     distinct = sum(lv.new for lv in levels)
