@@ -1,24 +1,39 @@
 #!/usr/bin/env python3
-"""bench.py -- distinct states/sec to exhaust a bounded 3-server Raft model.
-
-A "step" is one complete model check of the workload: clear the fingerprint
-set, Init, then BFS levels until no new state (TLC's "0 states left on
-queue").  value = distinct states / mean wall time per step, the wall time
-to exhaust being ms_per_step.  All inputs are device-resident (the search
-starts from the Init row); nothing crosses PCIe inside a level except an
-~100-byte counter read-back.
+"""bench.py -- distinct states/sec of the BFS over raft.tla's Next on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 
-N > 1 (launched by torch.distributed.run, one process per GPU): the search
-is partitioned by fingerprint ownership -- each rank owns 1/N of the
-fingerprint set, and every BFS level exchanges successor fingerprints with
-their owners over RCCL (all-to-all-v on xGMI).  The model is fixed, so the
-scaling is strong; value is the whole job's distinct states / wall time.
+Workloads:
+
+* ``cfg2`` (default) -- BASELINE.json configs[1] exactly as stated: 3 servers,
+  Value = {v1, v2}, currentTerm <= 3, Len(log) <= 2, <= 1 copy per message,
+  ElectionSafety + LogMatching, NO in-flight bound.  Its state space grows ~3x
+  per BFS level and does not fit one GPU (nor TLC), so the search runs until
+  device memory is full: a sizing run finds the deepest level whose next level
+  no longer fits (the row arena, the fingerprint set or the row format runs
+  out -- reported, never truncated), then every timed step is a BFS from Init
+  through exactly those complete levels.  value = distinct states found /
+  wall time per step; ``exhausted`` is false and ``levels`` / ``distinct``
+  say how far it got.
+* ``cfg1`` -- BASELINE.json configs[0], the bounds of the reference's raft.cfg
+  (3 servers, one value, term <= 2, log <= 1, 1 copy), NoTwoLeaders; capped
+  the same way.
+* ``raft3_v2_t2_l2_m2`` and friends -- exhaustible analogues with a
+  MaxInFlight bound (specs/MC.tla): a step is a complete model check (TLC's
+  "0 states left on queue"), ms_per_step is the wall time to exhaust.  The
+  default run adds this as the secondary ``exhaust`` object.
+
+A "step" starts from the Init row on the device: no input crosses PCIe
+inside the timed region except ~200-byte counter read-backs per level.
+
+N > 1: one process per GPU (bench.py re-launches itself under
+torch.distributed.run when WORLD_SIZE is unset), the search partitioned by
+fingerprint ownership over RCCL (all-to-all-v on xGMI every level).
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -26,18 +41,29 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raft-tla_amd"))
 
-# Feasible analogues of BASELINE.json configs (the reference's bounds give
-# >1e11 states): name -> (N, V, MaxTerm, MaxLogLen, MaxCopies, MaxInFlight, invariants)
+ES_LM = ("ElectionSafety", "LogMatching")
+# name -> (N, V, MaxTerm, MaxLogLen, MaxCopies, MaxInFlight, invariants)
 WORKLOADS = {
-    "raft3_v2_t2_l2_m2": (3, 2, 2, 2, 1, 2, ("ElectionSafety", "LogMatching")),
-    "raft3_v2_t2_l1_m3": (3, 2, 2, 1, 1, 3, ("ElectionSafety", "LogMatching")),
-    "raft3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, ("ElectionSafety", "LogMatching")),
+    "cfg2": (3, 2, 3, 2, 1, 0, ES_LM),                     # BASELINE.json configs[1]
+    "cfg1": (3, 1, 2, 1, 1, 0, ("NoTwoLeaders",)),         # BASELINE.json configs[0] (raft.cfg bounds)
+    "raft3_v2_t2_l2_m2": (3, 2, 2, 2, 1, 2, ES_LM),
+    "raft3_v2_t2_l1_m3": (3, 2, 2, 1, 1, 3, ES_LM),
+    "raft3_v2_t2_l1_m2": (3, 2, 2, 1, 1, 2, ES_LM),
     "raft3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, ("NoTwoLeaders",)),
     "raft3_v1_t2_l1_m1": (3, 1, 2, 1, 1, 1, ("NoTwoLeaders",)),
 }
-DEFAULT = "raft3_v2_t2_l2_m2"
-# fingerprint-set size per workload (distinct states: 2.41e9, 2.54e9, 1.45e8)
-FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30}
+BASELINE_INDEX = {"cfg1": 0, "cfg2": 1}
+CAPPED = {"cfg1", "cfg2"}          # not exhaustible on one GPU: run until HBM is full
+DEFAULT = "cfg2"
+SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run reports it too)
+# Fingerprint-set size (log2 slots) per workload: ~25-30 % load at the size reached.
+FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30,
+              "cfg2": 31, "cfg1": 31}
+# Bag slots per row for the unbounded-bag configs.  A state d BFS levels below
+# Init holds at most d - 1 distinct messages (every action adds at most one),
+# so this bounds the depth at which the row format -- not memory -- stops the
+# search; a successor that needs more raises RTLA_CAP_ROW, never truncates.
+BAG_CAP = {"cfg2": 18, "cfg1": 24}
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Random 8-byte fingerprint-set accesses into a 32 GiB table (far beyond the
 # 256 MiB Infinity Cache), all CUs, measured on MI355X by tools/probe_calib.py
@@ -49,7 +75,7 @@ CAS_PER_S = 1.55e10
 LOAD_PER_S = 4.66e10
 
 
-def load_traffic(workload, launches):
+def load_traffic(workload):
     """HBM bytes of the probe kernel per launch from the committed PMC profile
     (profiles/*/traffic.json, written by tools/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this workload), or None."""
@@ -69,9 +95,11 @@ def load_traffic(workload, launches):
 def fpset_log2_for(workload, world, override=0):
     """log2 fingerprint-set slots per rank: the workload's single-GPU size,
     divided by the next power of two >= world (each rank owns 1/world of the
-    fingerprints, so the load stays ~28 %); an explicit override is per rank."""
+    fingerprints, so the load stays ~28 %); an explicit override is per rank.
+    Capped workloads keep the single-GPU size per rank: with more GPUs they
+    reach deeper levels."""
     fpl = override or FPSET_LOG2.get(workload, 30)
-    if not override and world > 1:
+    if not override and world > 1 and workload not in CAPPED:
         fpl = max(24, fpl - (world - 1).bit_length())
     return fpl
 
@@ -101,6 +129,30 @@ def dist_env():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc, argv):
+    """--gpus N without a launcher: run N ranks of this script under
+    torch.distributed.run as a CHILD process (nothing here has touched the
+    GPU, and the parent never execs), relay its output and exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: every CPU this process may run on."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(shape, sample_states, threads):
     """The C oracle (oracle/raft_cpu.c, a 'port' of the spec) on a bounded
     prefix of the same BFS: distinct states/s on the host cores."""
@@ -109,84 +161,84 @@ def cpu_baseline(shape, sample_states, threads):
     n, v, t, l, c, m, inv = shape
     r = raft_cpu.bfs(raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=sample_states), threads=threads)
     return {"value": r["distinct"] / r["seconds"], "unit": "distinct states/s", "cores": threads,
-            "kind": "port",
-            "sample": "oracle/raft_cpu.c BFS of the same model, first %d levels (%d distinct, %d generated) in %.1f s"
-                      % (len(r["levels"]), r["distinct"], r["generated"], r["seconds"])}
+            "host_cpus": os.cpu_count(), "kind": "port", "levels": len(r["levels"]),
+            "sample": "prefix rate: oracle/raft_cpu.c level-synchronous BFS of the same model, first %d levels "
+                      "(%d distinct, %d generated) in %.1f s on %d threads"
+                      % (len(r["levels"]), r["distinct"], r["generated"], r["seconds"], threads)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default=DEFAULT, choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-sample", type=int, default=12_000_000, help="states in the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--fpset-log2", type=int, default=0,
-                    help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the "
-                         "workload (2^33 slots = 64 GiB for the 2.4e9-state default at 28%% load: 11%% faster "
-                         "than 2^32 at 56%%, fewer long probe chains per wave, tools/fpset_sweep.sh; 2^34 leaves "
-                         "too little HBM for the frontiers; fewer per rank when sharded)")
-    ap.add_argument("--levels", action="store_true", help="print the per-level table to stderr")
-    ap.add_argument("--shards", type=int, default=0,
-                    help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
-                         "(the multi-GPU exchange protocol with device copies as transport)")
-    args = ap.parse_args()
+class Run:
+    """A checker context for one workload, and how to time it."""
 
-    rank, world, local = dist_env()
-    import rtla
-    comm_id = None
-    if world > 1:
-        import torch.distributed as dist
-        # gloo = control plane only (RCCL id broadcast, barriers, max-reduce of
-        # times); the data path is the library's own RCCL communicator.
-        dist.init_process_group("gloo")
-        comm_id = share_comm_id(rank, rtla.comm_id)
+    def __init__(self, rtla, name, rank, world, comm_id, args, frontier_cap=0):
+        self.rtla = rtla
+        self.name = name
+        self.shape = WORKLOADS[name]
+        self.capped = name in CAPPED
+        n, v, t, l, c, m, inv = self.shape
+        self.fpl = fpset_log2_for(name, world, args.fpset_log2)
+        self.cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=self.fpl, shards=args.shards,
+                               bag_cap=BAG_CAP.get(name, 0), frontier_cap=frontier_cap,
+                               mem_budget=(200 << 30) if args.shards > 1 else 0)
+        self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
+        self.levels_cap = None   # complete levels a capped search reaches
+        self.stop = None         # what stopped the sizing run
 
-    shape = WORKLOADS[args.workload]
-    n, v, t, l, c, m, inv = shape
-    fpl = fpset_log2_for(args.workload, world, args.fpset_log2)
-    cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=fpl, shards=args.shards,
-                      mem_budget=(200 << 30) if args.shards > 1 else 0)
-    ck = rtla.Checker(cfg, rank=rank, world=world, comm_id=comm_id)
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-
-    def one_run():
+    def size(self):
+        """Capped workloads: BFS until the next level does not fit; the timed
+        steps then run exactly the complete levels before it."""
+        ck = self.ck
         ck.reset()
-        ck.run()
-        if ck.status < 0 or ck.status == rtla.VIOLATION:
-            raise SystemExit("model check ended with status %d" % ck.status)
+        st = ck.init()
+        while st == self.rtla.OK:
+            try:
+                st = ck.step()
+            except self.rtla.RtlaError as e:
+                if e.status != -3:  # only capacity may stop a capped search
+                    raise
+                self.stop = str(e)
+                break
+        if st == self.rtla.VIOLATION:
+            raise SystemExit("%s: invariant violated" % self.name)
+        self.levels_cap = len(ck.levels)
+        self.exhausted = st == self.rtla.DONE
+
+    def one(self):
+        ck = self.ck
+        ck.reset()
+        if self.capped:
+            st = ck.init()
+            while st == self.rtla.OK and len(ck.levels) < self.levels_cap:
+                st = ck.step()
+        else:
+            st = ck.run()
+        if st < 0 or st == self.rtla.VIOLATION:
+            raise SystemExit("%s: model check ended with status %d" % (self.name, st))
         return ck.levels
 
-    for _ in range(args.warmup):
-        one_run()
+
+def timed(run, steps, warmup, world, barrier):
+    if run.capped:
+        run.size()
+    for _ in range(warmup):
+        run.one()
     barrier()
     t0 = time.perf_counter()
-    runs = []
-    for _ in range(args.steps):
-        runs.append(one_run())
+    levels = None
+    for _ in range(steps):
+        levels = run.one()
     t1 = time.perf_counter()
     barrier()
-    elapsed = max_over_ranks(t1 - t0, world)
+    return max_over_ranks(t1 - t0, world) / steps, levels
 
-    levels = runs[-1]
-    distinct = sum(lv.new for lv in levels)
-    generated = sum(lv.generated for lv in levels)
-    depth = sum(1 for lv in levels if lv.new > 0)
-    per_step = elapsed / args.steps
-    value = distinct / per_step
 
-    # Roofline of the dominant kernel, the probe kernel k_expand_compact, from
-    # the last run's HIP-event times (expand_ms: the probe kernel alone; the
-    # rest of kernel_ms is k_materialize building the new rows).
-    # Algorithmic bytes of one launch over E frontier states: E*S (rows read)
-    # + P*64 (one 64-B HBM transaction per fingerprint-set probe, P in-model
-    # successors that differ from their parent) + D*8 (parent records).
+def roofline(levels, world, workload):
+    """Roofline of the dominant kernel, the probe kernel k_expand_compact,
+    from the last run's HIP-event times (expand_ms: the probe kernel alone;
+    the rest of kernel_ms is k_materialize building the new rows).
+    Algorithmic bytes of one launch over E frontier states: E*S (rows read)
+    + P*64 (one 64-B HBM transaction per fingerprint-set probe, P in-model
+    successors that differ from their parent) + D*8 (parent records)."""
     S = levels[0].row_bytes
     lv1 = levels[1:]
     launches = len(lv1)
@@ -199,60 +251,157 @@ def main():
     achieved = probe_kernel_bytes / world / (ems / 1e3) / 1e9   # per GPU
     mat_ms = kms - ems
     mat_bytes = D * (2 * S + 8)  # parent row read + record read + row written
-    traffic = load_traffic(args.workload, launches) if world == 1 else None
+    traffic = load_traffic(workload) if world == 1 else None
     ra_ceiling = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
-    if args.levels and rank == 0:
-        for lv in levels:
-            print("level %3d frontier %12d new %12d generated %13d kernel %9.3f ms (probe %9.3f ms)" %
-                  (lv.level, lv.frontier, lv.new, lv.generated, lv.kernel_ms, lv.expand_ms), file=sys.stderr)
+    return {
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic["bytes_per_launch"] if traffic else None,
+        "traffic_source": traffic["source"] if traffic else None,
+        "kernel": "k_expand_compact", "launches": launches, "kernel_ms_total": ems,
+        "kernel_ms_avg": ems / max(1, launches),
+        "bytes_per_launch": probe_kernel_bytes / max(1, launches),
+        "bytes_per_frontier_state": probe_kernel_bytes / max(1, E),
+        "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + 8 B per new parent record",
+        "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
+                          "frac": P / world / (ems / 1e3) / ra_ceiling,
+                          "model": "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S)",
+                          "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)"},
+        "k_materialize": {"ms_total": mat_ms, "bytes": mat_bytes,
+                          "GB_per_s": mat_bytes / world / (mat_ms / 1e3) / 1e9 if mat_ms > 0 else None},
+    }
 
+
+def print_levels(name, levels):
+    for lv in levels:
+        print("%s level %3d frontier %12d new %12d generated %13d kernel %9.3f ms (probe %9.3f ms)" %
+              (name, lv.level, lv.frontier, lv.new, lv.generated, lv.kernel_ms, lv.expand_ms), file=sys.stderr)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default=DEFAULT, choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="distinct states in the CPU baseline sample (0 = per workload, ~10-30 s of CPU work)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary wall-time-to-exhaust line of the default run")
+    ap.add_argument("--fpset-log2", type=int, default=0,
+                    help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the workload")
+    ap.add_argument("--frontier-cap", type=int, default=0, help="rows of the frontier arena per rank (0 = auto)")
+    ap.add_argument("--levels", action="store_true", help="print the per-level tables to stderr")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / rendezvous check only: every rank joins the process group, receives rank 0's "
+                         "RCCL-id payload, prints one line and exits (no GPU work; used by the CPU tests)")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
+                         "(the multi-GPU exchange protocol with device copies as transport)")
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            cid = share_comm_id(rank, lambda: bytes(range(128)))
+            dist.barrier()
+            dist.destroy_process_group()
+        else:
+            cid = bytes(range(128))
+        print("bench.py rank %d of %d ready (id %s)" % (rank, world, cid[:4].hex()), flush=True)
+        return
+    import rtla
+    comm_id = None
+    if world > 1:
+        import torch.distributed as dist
+        # gloo = control plane only (RCCL id broadcast, barriers, max-reduce of
+        # times); the data path is the library's own RCCL communicator.
+        dist.init_process_group("gloo")
+        comm_id = share_comm_id(rank, rtla.comm_id)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    run = Run(rtla, args.workload, rank, world, comm_id, args, args.frontier_cap)
+    info = json.loads(run.ck.device_info())
+    per_step, levels = timed(run, args.steps, args.warmup, world, barrier)
+    distinct = sum(lv.new for lv in levels)
+    generated = sum(lv.generated for lv in levels)
+    depth = sum(1 for lv in levels if lv.new > 0)
+    if args.levels and rank == 0:
+        print_levels(args.workload, levels)
+    n, v, t, l, c, m, inv = run.shape
+    config = {
+        "workload": args.workload,
+        "baseline_config": BASELINE_INDEX.get(args.workload),
+        "servers": n, "values": v, "max_term": t, "max_log": l, "max_copies": c, "max_in_flight": m,
+        "invariants": list(inv), "distinct": distinct, "generated": generated, "depth": depth,
+        "exhausted": (not run.capped) or bool(run.exhausted), "levels": len(levels),
+        "parallelism": "single" if world == 1 else "fp-sharded%d" % world,
+        "fpset_slots_log2": run.fpl, "bag_cap": run.cfg.bag_cap or None,
+        "frontier_arena_rows": info.get("frontier_cap"), "row_bytes": levels[0].row_bytes,
+        "rccl_ranks": info.get("world"),
+    }
+    if run.capped:
+        config["stopped_by"] = run.stop
     out = {
         "metric": "distinct states/sec (whole node) + wall time to exhaust, 3-server Raft",
-        "value": value,
+        "value": distinct / per_step,
         "unit": "distinct states/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": per_step * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if run.capped else "strong",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "exhaustive BFS from Init (no input data)",
-        "config": {
-            "workload": args.workload,
-            "servers": n, "values": v, "max_term": t, "max_log": l, "max_copies": c, "max_in_flight": m,
-            "invariants": list(inv), "distinct": distinct, "generated": generated, "depth": depth,
-            "parallelism": "single" if world == 1 else "fp-sharded%d" % world,
-            "fpset_slots_log2": fpl,
-        },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "traffic_source": traffic["source"] if traffic else None,
-            "kernel": "k_expand_compact", "launches": launches, "kernel_ms_total": ems,
-            "kernel_ms_avg": ems / max(1, launches),
-            "bytes_per_launch": probe_kernel_bytes / max(1, launches),
-            "bytes_per_frontier_state": probe_kernel_bytes / max(1, E),
-            "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + 8 B per new parent record",
-            "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
-                              "frac": P / world / (ems / 1e3) / ra_ceiling,
-                              "model": "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S)",
-                              "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)"},
-            "k_materialize": {"ms_total": mat_ms, "bytes": mat_bytes,
-                              "GB_per_s": mat_bytes / world / (mat_ms / 1e3) / 1e9 if mat_ms > 0 else None},
-        },
+        "data": "BFS from the Init row (no input data)" + (
+            ", capped at the deepest level that fits device memory" if run.capped else ", exhaustive"),
+        "config": config,
+        "roofline": roofline(levels, world, args.workload),
         "cpu_baseline": None,
     }
+    run.ck.close()
+
+    if args.workload == DEFAULT and not args.no_secondary:
+        sec = Run(rtla, SECONDARY, rank, world, comm_id, args)
+        sec_step, sec_levels = timed(sec, args.steps, args.warmup, world, barrier)
+        if args.levels and rank == 0:
+            print_levels(SECONDARY, sec_levels)
+        d2 = sum(lv.new for lv in sec_levels)
+        out["exhaust"] = {"workload": SECONDARY, "shape": list(WORKLOADS[SECONDARY][:6]),
+                          "wall_s_to_exhaust": sec_step, "distinct": d2,
+                          "generated": sum(lv.generated for lv in sec_levels),
+                          "depth": sum(1 for lv in sec_levels if lv.new > 0),
+                          "distinct_per_s": d2 / sec_step,
+                          "probe_kernel": roofline(sec_levels, world, SECONDARY)}
+        sec.ck.close()
+
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline(shape, args.cpu_sample, args.cpu_threads)
+            sample = args.cpu_sample or (20_000_000 if run.capped else 12_000_000)
+            cb = cpu_baseline(run.shape, sample, args.cpu_threads or cpu_threads())
+            k = cb["levels"]  # the GPU's own rate over the same prefix of levels, for comparison
+            if k <= len(levels):
+                gsec = sum(lv.seconds for lv in levels[:k])
+                cb["gpu_same_prefix_value"] = sum(lv.new for lv in levels[:k]) / gsec if gsec > 0 else None
+            out["cpu_baseline"] = cb
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ck.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 2
+#define RTLA_ABI_VERSION 3
 
 /* status codes */
 #define RTLA_OK 0
@@ -81,7 +81,9 @@ typedef struct {
     int32_t shards;      /* world == 1 only: split the search on this GPU into this many
                             fingerprint-owned shards (same exchange protocol as multi-GPU,
                             transport = device copies); 0/1 = one shard */
-    uint64_t frontier_cap; /* states per frontier buffer; 0 = auto */
+    uint64_t frontier_cap; /* rows of the frontier arena (current + next level, used as a ring;
+                              rounded down to a multiple of 64); 0 = all HBM left after the other
+                              structures */
     uint64_t mem_budget;   /* bytes of HBM this context may use; 0 = 85% of free */
     uint64_t chunk;        /* multi-shard: frontier states expanded per exchange round; 0 = auto */
 } rtla_cfg;
@@ -99,7 +101,17 @@ typedef struct {
     uint64_t probes;          /* in-model successors (fingerprint-set probes) */
     uint64_t row_bytes;       /* bytes of one packed state row */
     double expand_ms;         /* of kernel_ms: the probe kernel alone (one shard); the rest builds the rows */
+    int32_t flags;            /* on RTLA_E_OVERFLOW / RTLA_E_SPEC: which capacity ran out (RTLA_CAP_*);
+                                 the level is then incomplete and the search cannot continue */
+    int32_t reserved;
 } rtla_level_stats;
+
+/* rtla_level_stats.flags */
+#define RTLA_CAP_SPEC_ERROR 1     /* TLC evaluation error in Next (index outside DOMAIN) */
+#define RTLA_CAP_ROW 2            /* bag_cap / elec_cap of the row format */
+#define RTLA_CAP_FRONTIER 4       /* row arena (current + next level) */
+#define RTLA_CAP_FPSET 8          /* fingerprint set probe limit */
+#define RTLA_CAP_OUTBOX 16        /* multi-shard exchange outbox */
 
 /* Library / context lifetime.  world > 1: `comm_id` is the 128-byte RCCL
  * unique id shared by all ranks (rank 0 makes it with rtla_comm_id). */

@@ -24,6 +24,7 @@
 #include <time.h>
 
 #include <chrono>
+#include <filesystem>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -387,8 +388,10 @@ int main(int argc, char** argv) {
     if (st < 0) break;
     if (ckpt_minutes > 0 && st == RTLA_OK &&
         std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count() >= ckpt_minutes * 60) {
-      std::string dir = ckpt_prefix.substr(0, ckpt_prefix.rfind('/'));
-      if (ckpt_prefix.find('/') != std::string::npos) (void)!system(("mkdir -p '" + dir + "'").c_str());
+      // in-process (no shell from a GPU-initialised process)
+      std::error_code ec;
+      if (ckpt_prefix.find('/') != std::string::npos)
+        std::filesystem::create_directories(ckpt_prefix.substr(0, ckpt_prefix.rfind('/')), ec);
       printf("Checkpointing of run %s\n", ckpt_prefix.c_str());
       if (rtla_checkpoint(ctx, ckpt_prefix.c_str()) != RTLA_OK) printf("Warning: checkpoint failed\n");
       else printf("Checkpointing completed at (%s)\n", now_str().c_str());

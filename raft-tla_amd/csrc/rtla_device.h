@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/rtla.h"
 #include "rtla_model.h"
 
 namespace rtla {
@@ -19,12 +20,36 @@ enum {
   FLAG_OUTBOX_FULL = 16,    // exchange outbox region too small
   FLAG_BAD_INDEX = 32,      // RTLA_CHECKED builds: a global index outside its buffer
 };
+static_assert(FLAG_SPEC_ERROR == RTLA_CAP_SPEC_ERROR && FLAG_ROW_OVERFLOW == RTLA_CAP_ROW &&
+                  FLAG_FRONTIER_FULL == RTLA_CAP_FRONTIER && FLAG_FPSET_FULL == RTLA_CAP_FPSET &&
+                  FLAG_OUTBOX_FULL == RTLA_CAP_OUTBOX,
+              "rtla.h RTLA_CAP_* mirror the device flags");
+
+// Most shards in one job (one per GPU of an 8-GPU node, or virtual shards on
+// one device): the expand kernels keep per-owner outbox state in registers /
+// LDS sized by it, and rtla_open refuses more (RTLA_E_CONFIG).
+constexpr int SHARD_MAX = 8;
 
 // Fingerprint ownership across shards (ranks): low 32 bits of fp.a scaled to
 // [0, nshard).  The fingerprint-set home slot uses the TOP bits of fp.a, so
 // ownership and placement are independent.
 RTLA_HD int fp_owner(FP f, int nshard) {
   return (int)(((f.a & 0xffffffffull) * (unsigned long long)nshard) >> 32);
+}
+
+// A BFS level's rows inside the shard's row arena.  The arena (`cap` rows, a
+// multiple of 64) is used as a ring: state g of the level is row
+// (start + g) mod cap.  The next level starts at the first multiple of 64 past
+// the current one, so one level's rows never overlap the next level's, both
+// together may fill the whole arena (TLC's disk queue needs no second buffer
+// either), and a group of 64 states starting at a multiple of 64 never wraps.
+struct Ring {
+  uint32_t* base;
+  unsigned long long start, cap;
+};
+RTLA_HD unsigned long long ring_idx(const Ring& r, unsigned long long g) {
+  const unsigned long long i = r.start + g;  // start < cap and g < cap
+  return i >= r.cap ? i - r.cap : i;
 }
 
 // Outbox of one shard for one expansion chunk: region p (capacity `cap`
@@ -37,13 +62,12 @@ struct ShardBox {
   unsigned long long* send_ref;   // [nshard][cap]: local parent index << 16 | instance
 };
 
-// Diagnostic switches of k_expand_lane (rtla_time_expand only; 0 in the BFS).
+// Diagnostic switches of the expand kernels (rtla_time_expand, RTLA_XFLAGS; 0 in the BFS).
 enum {
   XF_NO_PROBE = 1,        // skip the fingerprint-set CAS (every successor "seen")
   XF_NO_COVER = 2,        // skip the coverage counters
   XF_NO_HASH = 4,         // replace the fingerprint delta by a trivial sum
   XF_NO_MATERIALIZE = 8,  // do not launch k_materialize
-  XF_LANE_KERNEL = 16,    // use k_expand_lane (no compaction) for a single shard
   XF_NO_CHUNKS = 32,      // compact kernel: load rows + per-state setup only
   XF_NO_DELTA = 64,       // compact kernel: compaction without evaluating actions
   XF_GENERIC_DELTA = 128, // compact kernel: never use the per-family specialised evaluation

@@ -6,7 +6,8 @@
 // buffer) and their parent pointers.  Device memory per shard:
 //   fingerprint set   2^fpset_log2 x 8 B   (open addressing, CAS insert)
 //   parents           one u64 per state: parent shard << 56 | parent index << 16 | instance
-//   frontier A / B    frontier_cap rows each (double buffer, swapped per level)
+//   row arena         frontier_cap rows (a multiple of 64), used as a ring: the
+//                     current level's rows, then the next level's after them
 //   outbox / inbox    (multi-shard only) per destination: fingerprints, refs, answers
 //
 // Deployments:
@@ -37,6 +38,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -59,8 +61,8 @@ struct Shard {
   uint64_t* table = nullptr;
   uint64_t* parents = nullptr;
   uint64_t parents_cap = 0;
-  uint32_t* front[2] = {nullptr, nullptr};
-  int cur = 0;
+  uint32_t* arena = nullptr;        // frontier rows: the current and the next level, as a ring (Ring)
+  uint64_t cur_start = 0;           // arena row of the current level's first state (a multiple of 64)
   uint64_t n_cur = 0, cur_base = 0;
   DevCounters* ctr = nullptr;
   int* dflags = nullptr;
@@ -109,6 +111,33 @@ struct rtla_ctx {
   int grid = 0;
   std::vector<uint32_t> init_row;
 };
+
+// ---- the row arena as a ring (Ring, rtla_device.h)
+static uint64_t round64(uint64_t n) { return (n + 63) & ~63ull; }
+static Ring cur_ring(const rtla_ctx* x, const Shard& s) { return Ring{s.arena, s.cur_start, x->front_cap}; }
+// The next level starts at the first 64-row boundary past the current one
+// and may use every arena row the current level does not.
+static Ring next_ring(const rtla_ctx* x, const Shard& s) {
+  return Ring{s.arena, (s.cur_start + round64(s.n_cur)) % x->front_cap, x->front_cap};
+}
+static uint64_t next_room(const rtla_ctx* x, const Shard& s) {
+  const uint64_t used = round64(s.n_cur);
+  return x->front_cap > used ? x->front_cap - used : 0;
+}
+// Copy states [g, g + n) of a level to / from the host (two pieces if they wrap).
+static hipError_t ring_copy(const Ring& r, int W, uint64_t g, uint64_t n, uint32_t* host, bool to_host) {
+  while (n) {
+    const uint64_t p = ring_idx(r, g), m = std::min<uint64_t>(n, r.cap - p);
+    uint32_t* dev = r.base + p * (uint64_t)W;
+    hipError_t e = to_host ? hipMemcpy(host, dev, m * W * 4, hipMemcpyDeviceToHost)
+                           : hipMemcpy(dev, host, m * W * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return e;
+    host += m * (uint64_t)W;
+    g += m;
+    n -= m;
+  }
+  return hipSuccess;
+}
 
 #define HIPCHK(x)                                                                                   \
   do {                                                                                              \
@@ -299,7 +328,7 @@ extern "C" int rtla_comm_id(void* out128) {
 }
 
 static void free_shard(Shard& s) {
-  void* ptrs[] = {s.table,    s.sent,     s.parents,  s.front[0], s.front[1], s.ctr,       s.dflags,    s.out_count,
+  void* ptrs[] = {s.table,    s.sent,     s.parents,  s.arena,    s.ctr,       s.dflags,    s.out_count,
                   s.in_count, s.all_count, s.send_fp, s.send_ref, s.send_ans,  s.recv_fp,   s.recv_ans,
                   s.new_count, s.all_new, s.rows_in,  s.rows_base, s.send_rows, s.recv_rows};
   for (void* p : ptrs)
@@ -333,12 +362,12 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   if (!x->front_cap) {
     uint64_t used = tbytes * (G > 1 ? 2 : 1) + pbytes + boxb;
     uint64_t rest = budget > used ? budget - used : 0;
-    x->front_cap = std::max<uint64_t>(rest / (2 * rowb), 1024);
+    x->front_cap = std::max<uint64_t>(rest / rowb, 2048);
   }
+  x->front_cap = std::max<uint64_t>(x->front_cap & ~63ull, 128);  // whole 64-row groups (Ring)
   HIPCHK(hipMalloc(&s.table, tbytes));
   HIPCHK(hipMalloc(&s.parents, pbytes));
-  HIPCHK(hipMalloc(&s.front[0], x->front_cap * rowb));
-  HIPCHK(hipMalloc(&s.front[1], x->front_cap * rowb));
+  HIPCHK(hipMalloc(&s.arena, x->front_cap * rowb));
   HIPCHK(hipMalloc(&s.ctr, sizeof(DevCounters)));
   HIPCHK(hipMalloc(&s.dflags, sizeof(int) * 64));
   if (G > 1) {
@@ -377,6 +406,7 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   *out = nullptr;
   if (world > 1 && !comm_id) return RTLA_E_ARG;
   if (world > 1 && cfg->shards > 1) return RTLA_E_CONFIG;
+  if (world > SHARD_MAX || cfg->shards > SHARD_MAX) return RTLA_E_CONFIG;  // per-owner outbox state is sized by it
   rtla_ctx* x = new rtla_ctx();
   x->cfg = *cfg;
   int r = layout_from_cfg(cfg, &x->L);
@@ -411,6 +441,7 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
       x->chunk = (per / 8) / ((uint64_t)G * nmax * 48);
       x->chunk = std::min<uint64_t>(std::max<uint64_t>(x->chunk, 1024), 4u << 20);
     }
+    x->chunk = round64(x->chunk);  // exchange rounds start at 64-row group boundaries (Ring)
     x->box_cap = x->chunk * nmax;
     // row regions: ~1/10 of the budget; winners beyond it ship in sub-rounds
     x->rows_cap = (per / 10) / (2ull * G * (L.W + 2) * 4);
@@ -465,7 +496,7 @@ static int env_xflags() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RTLA_XFLAGS");
-    v = e ? (atoi(e) & (XF_LANE_KERNEL | XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL)) : 0;
+    v = e ? (atoi(e) & (XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL)) : 0;
   }
   return v;
 }
@@ -535,6 +566,14 @@ bool file_to_dev(FILE* f, void* d, size_t n, std::vector<char>& buf) {
   }
   return true;
 }
+bool ring_to_file(FILE* f, const Ring& r, int W, uint64_t n, std::vector<char>& buf) {
+  for (uint64_t g = 0; g < n;) {
+    const uint64_t p = ring_idx(r, g), m = std::min<uint64_t>(n - g, r.cap - p);
+    if (!dev_to_file(f, r.base + p * (uint64_t)W, m * W * 4, buf)) return false;
+    g += m;
+  }
+  return true;
+}
 std::string ckpt_path(const char* prefix, int shard) {
   return std::string(prefix) + ".shard" + std::to_string(shard) + ".rtla";
 }
@@ -546,6 +585,10 @@ extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
   HIPCHK(hipSetDevice(x->device));
   HIPCHK(hipStreamSynchronize(x->stream));
   std::vector<char> buf(64 << 20);
+  // Each shard is written to <path>.tmp (flushed to disk); only when every
+  // shard of every rank has been written are the files renamed over the
+  // previous checkpoint, so a crash mid-write leaves the last good one intact.
+  uint64_t failed = 0;
   for (auto& s : x->sh) {
     CkptHeader h;
     memset(&h, 0, sizeof h);
@@ -556,18 +599,29 @@ extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
     h.cur_base = s.cur_base; h.n_cur = s.n_cur; h.parents_n = s.cur_base + s.n_cur;
     h.finished = x->finished; h.viol_mask = s.viol_mask; h.viol_in_model = s.viol_in_model;
     h.viol_inst = s.viol_inst; h.viol_parent = s.viol_parent; h.viol_child = s.viol_child;
-    const std::string path = ckpt_path(prefix, s.id);
-    FILE* f = fopen(path.c_str(), "wb");
-    if (!f) return RTLA_E_ARG;
+    const std::string tmp = ckpt_path(prefix, s.id) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) { failed = 1; break; }
     DevCounters c;
     bool ok = write_all(f, &h, sizeof h) && dev_to_file(f, s.table, 8ull << x->tlog2, buf) &&
               (!s.sent || dev_to_file(f, s.sent, 8ull << x->tlog2, buf)) &&
               dev_to_file(f, s.parents, 8 * h.parents_n, buf) &&
-              dev_to_file(f, s.front[s.cur], 4ull * x->L.W * s.n_cur, buf) &&
+              ring_to_file(f, cur_ring(x, s), x->L.W, s.n_cur, buf) &&
               hipMemcpy(&c, s.ctr, sizeof c, hipMemcpyDeviceToHost) == hipSuccess &&
               write_all(f, c.cover, sizeof c.cover);
+    ok = ok && fflush(f) == 0 && fsync(fileno(f)) == 0;
     ok = fclose(f) == 0 && ok;
-    if (!ok) return RTLA_E_ARG;
+    if (!ok) { failed = 1; break; }
+  }
+  int rc = allreduce_u64(x, &failed, 1, 1);
+  if (rc) return rc;
+  if (failed) {
+    for (auto& s : x->sh) (void)remove((ckpt_path(prefix, s.id) + ".tmp").c_str());
+    return RTLA_E_ARG;
+  }
+  for (auto& s : x->sh) {
+    const std::string path = ckpt_path(prefix, s.id);
+    if (rename((path + ".tmp").c_str(), path.c_str()) != 0) return RTLA_E_ARG;
   }
   return RTLA_OK;
 }
@@ -590,16 +644,25 @@ extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
     ok = ok && file_to_dev(f, s.table, 8ull << x->tlog2, buf) &&
          (!s.sent || file_to_dev(f, s.sent, 8ull << x->tlog2, buf)) &&
          file_to_dev(f, s.parents, 8 * h.parents_n, buf) &&
-         file_to_dev(f, s.front[0], 4ull * x->L.W * h.n_cur, buf) && read_all(f, c.cover, sizeof c.cover);
+         file_to_dev(f, s.arena, 4ull * x->L.W * h.n_cur, buf) && read_all(f, c.cover, sizeof c.cover);
     fclose(f);
     if (!ok) return RTLA_E_STATE;
     HIPCHK(hipMemcpy(s.ctr, &c, sizeof c, hipMemcpyHostToDevice));
     level = h.level;
-    s.cur = 0; s.cur_base = h.cur_base; s.n_cur = h.n_cur;
+    s.cur_start = 0; s.cur_base = h.cur_base; s.n_cur = h.n_cur;
     s.viol_mask = h.viol_mask; s.viol_in_model = h.viol_in_model; s.viol_inst = h.viol_inst;
     s.viol_parent = h.viol_parent; s.viol_child = h.viol_child;
     x->level = h.level; x->distinct = h.distinct; x->generated = h.generated; x->max_front = h.max_front;
     x->finished = h.finished != 0;
+  }
+  if (x->world > 1) {  // every rank must resume from the same level of the same search
+    uint64_t v[6] = {(uint64_t)x->level, x->distinct, x->generated, ~(uint64_t)x->level, ~x->distinct, ~x->generated};
+    int rc = allreduce_u64(x, v, 6, 1);
+    if (rc) return rc;
+    if (v[0] != ~v[3] || v[1] != ~v[4] || v[2] != ~v[5]) {
+      fprintf(stderr, "rtla: checkpoint files of different ranks are from different levels\n");
+      return RTLA_E_STATE;
+    }
   }
   x->init_row.assign(x->L.W, 0);
   row_init(x->L, x->init_row.data());
@@ -614,7 +677,7 @@ extern "C" int rtla_reset(rtla_ctx* x) {
     HIPCHK(hipMemsetAsync(s.table, 0, 8ull << x->tlog2, x->stream));
     if (s.sent) HIPCHK(hipMemsetAsync(s.sent, 0, 8ull << x->tlog2, x->stream));
     HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
-    s.n_cur = 0; s.cur_base = 0; s.cur = 0;
+    s.n_cur = 0; s.cur_base = 0; s.cur_start = 0;
     s.viol_mask = 0; s.viol_in_model = 0; s.viol_inst = -1; s.viol_parent = 0; s.viol_child = ~0ull;
   }
   HIPCHK(hipStreamSynchronize(x->stream));
@@ -633,10 +696,10 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
   // Init belongs to the shard that owns its fingerprint (raft.tla:155-160: one state)
   int owner = fp_owner(row_fp(x->init_row.data()), x->nshard);
   for (auto& s : x->sh) {
-    s.cur = 0; s.cur_base = 0; s.n_cur = 0;
+    s.cur_start = 0; s.cur_base = 0; s.n_cur = 0;
     if (s.id != owner) continue;
-    HIPCHK(hipMemcpyAsync(s.front[0], x->init_row.data(), L.W * 4, hipMemcpyHostToDevice, x->stream));
-    HIPCHK(launch_insert_rows(L, s.front[0], 1, s.table, x->tlog2, s.dflags, s.ctr, x->stream));
+    HIPCHK(hipMemcpyAsync(s.arena, x->init_row.data(), L.W * 4, hipMemcpyHostToDevice, x->stream));
+    HIPCHK(launch_insert_rows(L, s.arena, 1, s.table, x->tlog2, s.dflags, s.ctr, x->stream));
     uint64_t root = ~0ull;
     HIPCHK(hipMemcpyAsync(s.parents, &root, 8, hipMemcpyHostToDevice, x->stream));
     s.n_cur = 1;
@@ -814,11 +877,11 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   for (size_t k = 0; k < x->sh.size(); k++) {
     Shard& s = x->sh[k];
     HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
-    s.h_caps[0] = x->front_cap; s.h_caps[1] = x->front_cap; s.h_caps[2] = s.parents_cap;
-    HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
     next_base[k] = s.cur_base + s.n_cur;
     if (next_base[k] >= s.parents_cap) return RTLA_E_OVERFLOW;
-    next_cap[k] = std::min<uint64_t>(x->front_cap, s.parents_cap - next_base[k]);
+    next_cap[k] = std::min<uint64_t>(next_room(x, s), s.parents_cap - next_base[k]);
+    s.h_caps[0] = s.n_cur; s.h_caps[1] = next_cap[k]; s.h_caps[2] = s.parents_cap;
+    HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
   }
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev0, x->stream));
   if (G == 1) {
@@ -827,7 +890,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     uint64_t blocks = (s.n_cur + 3) / 4;
     int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
     HIPCHK(hipEventRecord(s.evm, x->stream));  // (re-recorded between the kernels when k_materialize runs)
-    HIPCHK(launch_expand(L, s.front[s.cur], 0, s.n_cur, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[0],
+    HIPCHK(launch_expand(L, cur_ring(x, s), 0, s.n_cur, s.cur_base, next_ring(x, s), s.parents, next_base[0],
                          next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), nullptr, s.evm));
   } else {
     // lock-step chunks over the frontier; every shard runs the same number
@@ -842,7 +905,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
                      (unsigned long long*)s.send_fp, (unsigned long long*)s.send_ref};
         uint64_t blocks = (e - b + 3) / 4;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), (uint64_t)x->grid);
-        HIPCHK(launch_expand(L, s.front[s.cur], b, e, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base[k],
+        HIPCHK(launch_expand(L, cur_ring(x, s), b, e, s.cur_base, next_ring(x, s), s.parents, next_base[k],
                              next_cap[k], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), s.sent));
       }
       int rc = gather_counts(x);
@@ -864,7 +927,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
           Shard& s = x->sh[k];
           uint64_t mx_out = 0;
           for (uint64_t v : s.h_out) mx_out = std::max(mx_out, v);
-          HIPCHK(launch_pack_rows(L, s.front[s.cur], s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
+          HIPCHK(launch_pack_rows(L, cur_ring(x, s), s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
                                   x->box_cap, lo, lo + x->rows_cap, s.send_rows, x->rows_cap, s.ctr, mx_out,
                                   x->stream));
         }
@@ -874,7 +937,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
           Shard& s = x->sh[k];
           uint64_t mx_rows = 0;
           for (uint64_t v : s.h_new_in) mx_rows = std::max(mx_rows, v > lo ? std::min(v - lo, x->rows_cap) : 0);
-          HIPCHK(launch_unpack_rows(L.W, s.recv_rows, s.rows_in, s.rows_base, G, x->rows_cap, s.front[s.cur ^ 1],
+          HIPCHK(launch_unpack_rows(L.W, s.recv_rows, s.rows_in, s.rows_base, G, x->rows_cap, next_ring(x, s),
                                     s.parents, next_base[k], next_cap[k], s.ctr, mx_rows, x->stream));
         }
       }
@@ -909,7 +972,17 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   int rc = allreduce2_u64(x, sums, 4, maxs, 4);
   if (rc) return rc;
   x->max_front = maxs[3];
-  if (maxs[0]) { report_flags((int)maxs[0]); x->finished = true; return flags_to_status((int)maxs[0]); }
+  if (maxs[0]) {
+    report_flags((int)maxs[0]);
+    x->finished = true;
+    if (st) {  // the level is incomplete: only which capacity ran out is reported
+      memset(st, 0, sizeof *st);
+      st->level = x->level + 1; st->status = flags_to_status((int)maxs[0]); st->flags = (int32_t)maxs[0];
+      st->frontier = sums[3]; st->distinct_total = x->distinct; st->generated_total = x->generated;
+      st->row_bytes = (uint64_t)L.W * 4; st->seconds = now_s() - t0;
+    }
+    return flags_to_status((int)maxs[0]);
+  }
   uint64_t nnew = sums[0];
   x->generated += sums[1];
   x->distinct += nnew;
@@ -925,8 +998,8 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   for (size_t k = 0; k < x->sh.size(); k++) {
     Shard& s = x->sh[k];
     s.cur_base = next_base[k];
+    s.cur_start = next_ring(x, s).start;
     s.n_cur = hc[k].next_count;
-    s.cur ^= 1;
   }
   if (st) {
     memset(st, 0, sizeof *st);
@@ -965,7 +1038,7 @@ extern "C" int rtla_frontier(rtla_ctx* x, uint32_t* rows, size_t cap, size_t* n)
   size_t off = 0;
   for (auto& s : x->sh) {
     if (s.n_cur)
-      HIPCHK(hipMemcpy(rows + off * x->L.W, s.front[s.cur], (size_t)s.n_cur * x->L.W * 4, hipMemcpyDeviceToHost));
+      HIPCHK(ring_copy(cur_ring(x, s), x->L.W, 0, s.n_cur, rows + off * x->L.W, true));
     off += s.n_cur;
   }
   return RTLA_OK;
@@ -1085,13 +1158,13 @@ extern "C" int rtla_time_expand(rtla_ctx* x, int xflags, int reps, double* ms) {
   Shard& s = x->sh[0];
   const uint64_t next_base = s.cur_base + s.n_cur;
   if (next_base >= s.parents_cap) return RTLA_E_OVERFLOW;
-  const uint64_t next_cap = std::min<uint64_t>(x->front_cap, s.parents_cap - next_base);
+  const uint64_t next_cap = std::min<uint64_t>(next_room(x, s), s.parents_cap - next_base);
   ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
   float total = 0.f;
   for (int r = 0; r < reps; r++) {
     HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
     HIPCHK(hipEventRecord(s.ev0, x->stream));
-    HIPCHK(launch_expand(x->L, s.front[s.cur], 0, s.n_cur, s.cur_base, s.front[s.cur ^ 1], s.parents, next_base,
+    HIPCHK(launch_expand(x->L, cur_ring(x, s), 0, s.n_cur, s.cur_base, next_ring(x, s), s.parents, next_base,
                          next_cap, s.table, x->tlog2, s.ctr, box, x->grid, x->stream, xflags));
     HIPCHK(hipEventRecord(s.ev1, x->stream));
     HIPCHK(hipEventSynchronize(s.ev1));

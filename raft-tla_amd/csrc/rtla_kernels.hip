@@ -58,20 +58,38 @@ __device__ __forceinline__ void copy_words_lds(uint32_t* __restrict__ dst, const
 }
 
 // Gather nv rows of W words (row r from src_row(r), a wave-uniform address)
-// into LDS rows dst + r * W, 8 rows in flight.  W <= 64: one word per lane.
+// into LDS rows dst + r * W: lane l moves words l, l + 64, ... of each row,
+// 8 rows (8 loads per lane) in flight.
 template <class F>
 __device__ __forceinline__ void gather_rows_lds(uint32_t* __restrict__ dst, int W, int nv, F src_row, int lane) {
-  if (W <= 64) {
-    for (int r0 = 0; r0 < nv; r0 += 8) {
+  for (int r0 = 0; r0 < nv; r0 += 8) {
+    for (int c = lane; c < W; c += 64) {
       uint32_t v[8];
 #pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = (r0 + j < nv && lane < W) ? src_row(r0 + j)[lane] : 0u;
+      for (int j = 0; j < 8; j++) v[j] = r0 + j < nv ? src_row(r0 + j)[c] : 0u;
 #pragma unroll
       for (int j = 0; j < 8; j++)
-        if (r0 + j < nv && lane < W) dst[(r0 + j) * W + lane] = v[j];
+        if (r0 + j < nv) dst[(r0 + j) * W + c] = v[j];
     }
-  } else {
-    for (int r = 0; r < nv; r++) copy_words_lds(dst + r * W, src_row(r), W, lane);
+  }
+}
+
+// Row pointer of state g of a level (see Ring, rtla_device.h).
+__device__ __forceinline__ uint32_t* ring_row(const Ring& R, unsigned long long g, int W) {
+  return R.base + ring_idx(R, g) * (unsigned long long)W;
+}
+
+// Store nr consecutive rows (LDS src, W words each) as states g .. g + nr - 1
+// of the level R, coalesced; the range may wrap at the end of the arena.
+__device__ __forceinline__ void store_rows_ring(const Ring& R, unsigned long long g, int nr, int W,
+                                                const uint32_t* __restrict__ src, int lane) {
+  const unsigned long long p = ring_idx(R, g);
+  const int n1 = (int)min<unsigned long long>(R.cap - p, (unsigned long long)nr) * W;  // words before the wrap
+  uint32_t* d1 = R.base + p * (unsigned long long)W;
+  const int nw = nr * W;
+  for (int w = lane; w < nw; w += 64) {
+    if (w < n1) d1[w] = src[w];
+    else R.base[w - n1] = src[w];
   }
 }
 
@@ -97,9 +115,12 @@ __device__ __forceinline__ void set_flag(DevCounters* c, int f) { atomicOr(&c->f
 // Slots only ever change 0 -> key, so a slot holding the key proves the
 // state is present, and one holding another key can be skipped for good;
 // only an empty slot needs the CAS (which may then find the key after all).
+// lossy (the MULTI sent cache, a dedup hint only): a long probe chain answers
+// "not sent yet" -- the record is shipped and its owner deduplicates -- and
+// never raises FLAG_FPSET_FULL.
 __device__ __forceinline__ bool fpset_resolve_loaded(unsigned long long* table, int log2, unsigned long long key,
                                                      unsigned long long idx, unsigned long long seen,
-                                                     DevCounters* ctr) {
+                                                     DevCounters* ctr, bool lossy = false) {
   const unsigned long long mask = (1ull << log2) - 1ull;
   for (int probe = 1;; probe++) {
     if (seen == key) return false;
@@ -108,6 +129,7 @@ __device__ __forceinline__ bool fpset_resolve_loaded(unsigned long long* table, 
       if (seen == 0ull) return true;
       if (seen == key) return false;
     }
+    if (lossy && probe >= 64) return true;
     if (probe >= 4096) {
       set_flag(ctr, FLAG_FPSET_FULL);
       return false;
@@ -208,8 +230,8 @@ __device__ __forceinline__ FP load_parent(const Layout& L, const uint32_t* __res
 
 template <int NS>
 __global__ void __launch_bounds__(256)
-k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
-         unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
+k_expand(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_end,
+         unsigned long long cur_base, Ring next, unsigned long long* __restrict__ parents,
          unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
          DevCounters* ctr, ShardBox box) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -232,7 +254,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
   for (int i = 2; i <= NS; i++) nperm *= i;
   for (unsigned long long s = s_begin + (unsigned long long)blockIdx.x * wpb + wave; s < s_end;
        s += (unsigned long long)gridDim.x * wpb) {
-    const FP pfp = load_parent<NS>(L, cur + s * (unsigned long long)W, prow, pall, hsrv, lane);
+    const FP pfp = load_parent<NS>(L, ring_row(cur, s, W), prow, pall, hsrv, lane);
     if (L.sym) {  // SYMMETRY: per-permutation fingerprints of the parent, lanes over permutations
       const FP afp = alllogs_fp(L, pall);  // allLogs' is the same for every successor (raft.tla:465)
       for (int k = lane; k < nperm; k += 64) {
@@ -317,9 +339,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
             if (isnew && rank >= b && rank < b + STAGE_ROWS)
               materialize<NS>(L, prow, d, pall, cfp, stage + (rank - b) * W);
             wave_sync();
-            const int nb = min(STAGE_ROWS, cnt - b);
-            uint32_t* dst = next + (obase + b) * (unsigned long long)W;
-            for (int w = lane; w < nb * W; w += 64) dst[w] = stage[w];
+            store_rows_ring(next, obase + b, min(STAGE_ROWS, cnt - b), W, stage, lane);
             wave_sync();
           }
           if (isnew)
@@ -349,27 +369,7 @@ k_expand(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin,
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
-// ------------------------------------------------------------------------
-// k_expand_lane: the BFS level kernel, one LANE per frontier state.
-//
-// A wave takes 64 consecutive frontier rows (one coalesced copy into LDS,
-// odd row stride W so lane-strided reads hit 64 distinct banks) and walks the
-// action-instance space q = 0..ncand-1 in lock-step: every lane evaluates the
-// SAME instance on its own state, so the family dispatch in compute_delta is a
-// uniform (scalar) branch and the wave never diverges across Next's
-// disjuncts.  Bag instances (Receive / Duplicate / Drop of slot k) run for
-// k < the wave's largest bag; lanes with fewer messages are simply disabled.
-//
-// Phase 1 (per chunk of 64 instances): delta, incremental fingerprint, one
-// CAS probe of the fingerprint set per in-model successor (skipped when the
-// successor equals its parent, which is already in the set), invariants on
-// new and out-of-model successors, coverage; new / remote successors are
-// remembered as one bit per (lane, instance).
-// Phase 2: ONE atomic reserves the whole wave's new rows (and one per
-// remote owner its records), then the flagged instances are re-derived and
-// materialised straight into the next frontier.  The reservation atomics
-// drop from one per state to one per 64 states: a single counter word
-// saturates at ~9e7 atomics/s on MI355X.
+// Helpers of the lane-per-state phases (k_expand_compact, k_materialize, k_pack_rows).
 namespace {
 
 struct LaneWords {  // word w of a per-lane array kept word-major (stride 64: bank-conflict free)
@@ -377,11 +377,6 @@ struct LaneWords {  // word w of a per-lane array kept word-major (stride 64: ba
   __device__ __forceinline__ uint32_t& operator[](int w) const { return p[w * 64]; }
 };
 
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-  return v;
-}
 __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
 #pragma unroll
@@ -391,245 +386,14 @@ __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) 
   }
   return (unsigned long long)lo | (unsigned long long)hi << 32;
 }
-// exclusive prefix sum over the wave; *total = the wave's sum (uniform)
-__device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  *total = __builtin_amdgcn_readlane(x, 63);
-  return x - v;
-}
-
-// q-th candidate of the wave -> instance id (uniform); *slot = bag slot or -1
-__device__ __forceinline__ int wave_inst(const Layout& L, int q, int fixed, int kmax) {
-  if (q < fixed) return q;
-  const int r = q - fixed, fam = r / kmax;
-  return fam_base(L, F_RECEIVE + fam) + (r - fam * kmax);
-}
-
-template <int NS>
-__device__ __forceinline__ FP sel_fp(const FP* h, int i) {
-  FP r{0, 0};
-#pragma unroll
-  for (int k = 0; k < NS; k++)
-    if (k == i) r = h[k];
-  return r;
-}
-
 __host__ __device__ constexpr int lane_lds_words(int W, int AW) { return 64 * W + 64 * AW; }
 
 }  // namespace
 
-#ifndef RTLA_LANE_WAVES_PER_EU
-#define RTLA_LANE_WAVES_PER_EU 1
-#endif
-template <int NS, bool MULTI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_LANE_WAVES_PER_EU)))
-k_expand_lane(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
-              unsigned long long cur_base, uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
-              unsigned long long next_base, unsigned long long next_cap, unsigned long long* table, int tlog2,
-              DevCounters* ctr, ShardBox box, int xflags) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ unsigned int cov[2 * COVER_CODES];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wpb = blockDim.x >> 6;
-  const int W = L.W, AW = L.all_words;
-  uint32_t* rows = lds + wave * lane_lds_words(W, AW);
-  const uint32_t* prow = rows + lane * W;
-  const LaneWords pall{rows + 64 * W + lane};
-  for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
-  __syncthreads();
-
-  unsigned my_gen = 0, my_probe = 0;
-  const int fixed = L.fam[F_RECEIVE];
-  const int G = MULTI ? box.nshard : 1;
-  for (unsigned long long s0 = s_begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; s0 < s_end;
-       s0 += (unsigned long long)gridDim.x * wpb * 64ull) {
-    const int nvalid = (int)min<unsigned long long>(64ull, s_end - s0);
-    {  // coalesced copy of the group's rows
-      const uint32_t* src = cur + s0 * (unsigned long long)W;
-      const int nw = nvalid * W;
-      for (int w = lane; w < nw; w += 64) rows[w] = src[w];
-    }
-    wave_sync();
-    const bool valid = lane < nvalid;
-    const unsigned long long s = s0 + lane;  // this lane's state
-    FP pfp0{0, 0}, pfp{0, 0};
-    int nmsg = 0;
-    if (valid) {
-      pfp0 = row_fp(prow);
-      pfp = fp_add(pfp0, alllogs_delta<NS>(L, prow, pall));
-      nmsg = row_nmsg(L, prow);
-    }
-    const int kmax = wave_max_i(nmsg);
-    const int ncand = fixed + 3 * kmax;
-    for (int base = 0; base < ncand; base += 64) {
-      const int qend = min(ncand, base + 64);
-      unsigned long long newm = 0, remm = 0;
-      int rcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      // ---- phase 1: evaluate and probe.  The CAS of instance q is resolved
-      // only after instance q+1's delta and fingerprint are computed, so
-      // every wave keeps one probe in flight behind its own arithmetic.
-      bool pend = false;
-      unsigned long long pold = 0, pkey = 0, pidx = 0;
-      int pbit = 0;
-      for (int q = base; q < qend; q++) {
-        const int inst = wave_inst(L, q, fixed, kmax);
-        DeltaFp d;
-        d.enabled = 0;
-        if (valid) compute_delta<NS>(L, prow, inst, d);
-        bool en = d.enabled != 0;
-        if (en && d.err) {
-          set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
-          en = false;
-        }
-        my_gen += en ? 1 : 0;
-        bool probe = false;
-        unsigned long long key = 0, idx = 0;
-        if (en && d.in_model) {
-          const FP cfp = (xflags & XF_NO_HASH) ? FP{pfp.a + d.rec[0] + (uint64_t)d.fmsg.a, pfp.b + d.rec[1]}
-                                                : fp_add(pfp, delta_fp<NS>(L, prow, d));
-          if (cfp.a != pfp0.a || cfp.b != pfp0.b) {  // successor == parent: already in the set
-            const int owner = MULTI ? fp_owner(cfp, G) : 0;
-            if (!MULTI || owner == box.me) {
-              probe = !(xflags & XF_NO_PROBE);
-              key = cfp.b | 1ull;
-              idx = cfp.a >> (64 - tlog2);
-            } else {
-              remm |= 1ull << (q - base);
-#pragma unroll
-              for (int o = 0; o < 8; o++) rcnt[o] += o == owner;
-            }
-          }
-        }
-        // generated coverage: the family is uniform; Receive's sub-action is per lane
-        if (xflags & XF_NO_COVER) {
-        } else if (q < fixed || (q - fixed) / kmax != 0) {
-          const int c1 = __popcll(__ballot(en));
-          if (lane == 0 && c1) atomicAdd(&cov[cover_code(L, inst, R_NONE)], (unsigned)c1);
-        } else {
-#pragma unroll
-          for (int sub = 0; sub < R_NONE; sub++) {
-            const int c1 = __popcll(__ballot(en && d.sub == sub));
-            if (lane == 0 && c1) atomicAdd(&cov[F_COUNT + sub], (unsigned)c1);
-          }
-        }
-        if (en && !d.in_model) {  // out-of-model successors: checked, never stored
-          const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-          if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-            ctr->viol_parent = cur_base + s;
-            ctr->viol_inst = inst;
-            ctr->viol_in_model = 0;
-            ctr->viol_child = ~0ull;
-          }
-        }
-        if (pend) {
-          if (fpset_resolve(table, tlog2, pkey, pidx, pold, ctr)) newm |= 1ull << pbit;
-        }
-        pend = probe;
-        if (probe) {
-          my_probe++;
-          pkey = key;
-          pidx = idx;
-          pbit = q - base;
-          pold = atomicCAS(&table[idx], 0ull, key);
-        }
-      }
-      if (pend) {
-        if (fpset_resolve(table, tlog2, pkey, pidx, pold, ctr)) newm |= 1ull << pbit;
-      }
-      // ---- phase 2: reserve, then materialise the flagged successors
-      int total = 0;
-      const int mine = __popcll(newm);
-      const int off = wave_excl_scan(mine, lane, &total);
-      unsigned long long obase = 0;
-      bool write_new = false;
-      if (total) {
-        if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)total);
-        obase = shfl0_u64(obase);
-        write_new = true;  // slots < next_cap are written below, the rest dropped (flagged)
-        if (obase + total > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
-      }
-      unsigned long long robase[8];
-      int roff[8];
-      bool any_rem = false;
-      if (MULTI) {
-#pragma unroll
-        for (int o = 0; o < 8; o++) {
-          int tot = 0;
-          roff[o] = o < G ? wave_excl_scan(rcnt[o], lane, &tot) : 0;
-          unsigned long long b = 0;
-          if (tot) {
-            any_rem = true;
-            if (lane == 0) b = atomicAdd(&box.out_count[o], (unsigned long long)tot);
-            b = shfl0_u64(b);
-          }
-          robase[o] = b;
-        }
-      }
-      // local new successors: only the parent record is written here;
-      // k_materialize builds the rows (its own launch, its own registers)
-      if (write_new) {
-        unsigned long long todo = wave_or_u64(newm);
-        int k_new = 0;
-        while (todo) {
-          const int bit = __builtin_ctzll(todo);
-          todo &= todo - 1;
-          if (newm >> bit & 1ull) {
-            const int inst = wave_inst(L, base + bit, fixed, kmax);
-            const unsigned long long slot = obase + off + k_new++;
-            if (slot < next_cap)
-              parents[next_base + slot] =
-                  (unsigned long long)box.me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
-          }
-        }
-      }
-      if (MULTI && any_rem) {  // successors owned by other shards: (fp, parent ref) records
-        unsigned long long todo = wave_or_u64(remm);
-        while (todo) {
-          const int bit = __builtin_ctzll(todo);
-          todo &= todo - 1;
-          if (!(remm >> bit & 1ull)) continue;
-          const int inst = wave_inst(L, base + bit, fixed, kmax);
-          DeltaFp d;
-          compute_delta<NS>(L, prow, inst, d);
-          const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
-          const int owner = fp_owner(cfp, G);
-          unsigned long long slot = 0;
-#pragma unroll
-          for (int o = 0; o < 8; o++)
-            if (o == owner) slot = robase[o] + (unsigned long long)roff[o]++;
-          if (slot < box.cap) {
-            const unsigned long long k = (unsigned long long)owner * box.cap + slot;
-            box.send_fp[2 * k] = cfp.a;
-            box.send_fp[2 * k + 1] = cfp.b;
-            box.send_ref[k] = s << 16 | (unsigned long long)inst;
-          } else {
-            set_flag(ctr, FLAG_OUTBOX_FULL);
-          }
-        }
-      }
-    }
-    wave_sync();  // the next group overwrites this group's rows
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    my_gen += __shfl_down(my_gen, off);
-    my_probe += __shfl_down(my_probe, off);
-  }
-  if (lane == 0 && my_gen) atomicAdd(&ctr->generated, (unsigned long long)my_gen);
-  if (lane == 0 && my_probe) atomicAdd(&ctr->probes, (unsigned long long)my_probe);
-  __syncthreads();
-  for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x)
-    if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
-}
-
 // ------------------------------------------------------------------------
 // k_expand_compact: the single-shard BFS level kernel with work compaction.
 //
-// Like k_expand_lane, a wave owns 64 frontier rows in LDS.  Each lane first
+// A wave owns 64 consecutive frontier rows in LDS.  Each lane first
 // computes, for its own state, the bit mask of action instances whose
 // enabling guard holds (the guards of raft.tla's actions, below).  The wave
 // then lists the (state, instance) pairs in instance-major order -- so
@@ -647,7 +411,7 @@ constexpr int NEWCAP = 128; // new-state list (u64 parent records)
 constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
 
 __host__ __device__ constexpr int compact_lds_words(int W, int AW) {
-  return 64 * W + 64 * AW + RING / 2 + 2 * NEWCAP + 4 * 8;  // + per-owner (base, used) of the open outbox chunk
+  return 64 * W + 64 * AW + RING / 2 + 2 * NEWCAP + 4 * SHARD_MAX;  // + per-owner (base, used) of the open outbox chunk
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -720,7 +484,7 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #endif
 template <int NS, bool MULTI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_COMPACT_WAVES_PER_EU)))
-k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long s_begin, unsigned long long s_end,
+k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_end,
                  unsigned long long cur_base, unsigned long long* __restrict__ parents, unsigned long long next_base,
                  unsigned long long next_cap, unsigned long long* table, unsigned long long* sent, int tlog2,
                  DevCounters* ctr, ShardBox box, int xflags) {
@@ -734,11 +498,11 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   const LaneWords pall_mine{rows + 64 * W + lane};
   uint16_t* ring = reinterpret_cast<uint16_t*>(rows + 64 * W + 64 * AW);
   unsigned long long* newl = reinterpret_cast<unsigned long long*>(rows + 64 * W + 64 * AW + RING / 2);
-  unsigned long long* obox = newl + NEWCAP;  // [o] = base of the open chunk, [8 + o] = slots used
+  unsigned long long* obox = newl + NEWCAP;  // [o] = base of the open chunk, [SHARD_MAX + o] = slots used
   if (MULTI) {
-    if (lane < 8) {
+    if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
-      obox[8 + lane] = OBOX_CHUNK;
+      obox[SHARD_MAX + lane] = OBOX_CHUNK;
     }
     wave_sync();
   }
@@ -775,9 +539,10 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   auto resolve = [&]() {
     bool isnew = false;
     if (pend) {
-      unsigned long long* t = (MULTI && powner != me) ? sent : table;
+      const bool to_sent = MULTI && powner != me;
+      unsigned long long* t = to_sent ? sent : table;
       isnew = (xflags & XF_CAS_ONLY) ? fpset_resolve(t, tlog2, pf.b | 1ull, pidx, pold, ctr)
-                                     : fpset_resolve_loaded(t, tlog2, pf.b | 1ull, pidx, pold, ctr);
+                                     : fpset_resolve_loaded(t, tlog2, pf.b | 1ull, pidx, pold, ctr, to_sent);
     }
     if (MULTI) {  // records for other owners: one outbox reservation per (wave, owner)
       const bool rem = isnew && powner != me;
@@ -788,7 +553,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
         om &= om - 1;
         const unsigned long long m = __ballot(rem && powner == o);
         const int cnt = __popcll(m);
-        unsigned long long b = obox[o], used = obox[8 + o];
+        unsigned long long b = obox[o], used = obox[SHARD_MAX + o];
         if (used + cnt > OBOX_CHUNK) {  // close the open chunk (holes = zero records), reserve the next
           if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
           unsigned long long nb = 0;
@@ -810,7 +575,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
         wave_sync();
         if (lane == 0) {
           obox[o] = b;
-          obox[8 + o] = used + cnt;
+          obox[SHARD_MAX + o] = used + cnt;
         }
         wave_sync();
       }
@@ -828,10 +593,10 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   for (unsigned long long s0 = s_begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; s0 < s_end;
        s0 += (unsigned long long)gridDim.x * wpb * 64ull) {
     const int nvalid = (int)min<unsigned long long>(64ull, s_end - s0);
-    {
-      const uint32_t* src = cur + s0 * (unsigned long long)W;
+    {  // s0 and cur.start are multiples of 64: the group's rows are contiguous in the arena
+      const uint32_t* src = ring_row(cur, s0, W);
       const int nw = nvalid * W;
-      if (RTLA_IDX_OK(ctr, s0 + nvalid, ctr->cap_cur + 1)) copy_words_lds(rows, src, nw, lane);
+      if (RTLA_IDX_OK(ctr, ring_idx(cur, s0) + nvalid, cur.cap + 1)) copy_words_lds(rows, src, nw, lane);
     }
     wave_sync();
     const bool valid = lane < nvalid;
@@ -969,7 +734,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
   if (nnew) flush_new();
   if (MULTI) {
     for (int o = 0; o < box.nshard; o++) {
-      const unsigned long long b = obox[o], used = obox[8 + o];
+      const unsigned long long b = obox[o], used = obox[SHARD_MAX + o];
       if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
     }
   }
@@ -984,7 +749,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
-// k_materialize: build the rows of the new states k_expand_lane found.
+// k_materialize: build the rows of the new states k_expand_compact found.
 // Slots [ctr->mat_begin, ctr->next_count) of the next frontier hold only a
 // parent record (shard << 56 | parent index << 16 | action instance); one
 // lane per slot stages its parent row in LDS, re-derives the successor with
@@ -992,7 +757,7 @@ k_expand_compact(Layout L, const uint32_t* __restrict__ cur, unsigned long long 
 // (raft.cfg:3, specs/MC.tla) and counts the distinct coverage.
 template <int NS>
 __global__ void __launch_bounds__(256)
-k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base, uint32_t* __restrict__ next,
+k_materialize(Layout L, Ring cur, unsigned long long cur_base, Ring next,
               const unsigned long long* __restrict__ parents, unsigned long long next_base,
               unsigned long long next_cap, DevCounters* ctr) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1019,7 +784,7 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
     // gather the parent rows: one coalesced row read per slot (rows stay in L2)
     gather_rows_lds(rows, W, nv, [&](int r) {
       const unsigned long long sr = readlane_u64(sidx, r);
-      return cur + (RTLA_IDX_OK(ctr, sr, ctr->cap_cur) ? sr : 0ull) * (unsigned long long)W;
+      return ring_row(cur, RTLA_IDX_OK(ctr, sr, ctr->cap_cur) ? sr : 0ull, W);
     }, lane);
     wave_sync();
     if (act) {
@@ -1038,12 +803,8 @@ k_materialize(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur
       materialize<NS>(L, prow, d, pall, cfp, prow);  // in place: the parent row is not read again
     }
     wave_sync();
-    {  // the group's rows are contiguous in the next frontier: coalesced stores
-      uint32_t* dst = next + g * (unsigned long long)W;
-      const int nw = nv * W;
-      if (RTLA_IDX_OK(ctr, g + nv, ctr->cap_next + 1))
-        for (int w = lane; w < nw; w += 64) dst[w] = rows[w];
-    }
+    // the group's rows are consecutive states of the next level: coalesced stores
+    if (RTLA_IDX_OK(ctr, g + nv, ctr->cap_next + 1)) store_rows_ring(next, g, nv, W, rows, lane);
     wave_sync();
   }
   __syncthreads();
@@ -1097,7 +858,7 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
 // action are known; a violation is recorded against the local parent.
 template <int NS>
 __global__ void __launch_bounds__(256)
-k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_base, int me,
+k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
             const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
             const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap, unsigned long long lo,
             unsigned long long hi, uint32_t* __restrict__ rows, unsigned long long rows_cap, DevCounters* ctr) {
@@ -1146,7 +907,7 @@ k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_b
     const bool act = lane < nw;
     const unsigned long long s = ref >> 16;
     const int inst = (int)(ref & 0xffffull);
-    gather_rows_lds(lrows, W, nw, [&](int r) { return cur + readlane_u64(s, r) * (unsigned long long)W; }, lane);
+    gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
     wave_sync();
     uint32_t* prow = lrows + lane * W;
     if (act) {
@@ -1187,7 +948,7 @@ k_pack_rows(Layout L, const uint32_t* __restrict__ cur, unsigned long long cur_b
 // row, coalesced copy) with their cross-shard parent records.
 __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ counts,
                               const unsigned long long* __restrict__ bases, int nshard, unsigned long long rows_cap,
-                              uint32_t* __restrict__ next, unsigned long long* __restrict__ parents,
+                              Ring next, unsigned long long* __restrict__ parents,
                               unsigned long long next_base, unsigned long long next_cap, DevCounters* ctr) {
   // grid.y = source shard p; its rows land at the contiguous slots bases[p] + k
   // (bases from k_part_counts: no per-row atomics)
@@ -1204,7 +965,7 @@ __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const un
       continue;
     }
     const uint32_t* src = rows + (p * rows_cap + k) * (unsigned long long)RW;
-    uint32_t* dst = next + o * (unsigned long long)W;
+    uint32_t* dst = ring_row(next, o, W);
     for (int w = lane; w < W; w += 64) dst[w] = src[w];
     if (lane == 0) parents[next_base + o] = (unsigned long long)src[W] | (unsigned long long)src[W + 1] << 32;
   }
@@ -1346,7 +1107,8 @@ static int device_cus() {
 
 int expand_compact_wpb(const Layout& L) {
   const size_t per = (size_t)compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-  if (per > 64 * 1024 || ((L.fam[F_COUNT] + 63) / 64) * 64 > 256) return 0;  // instance ids fit 8 bits per window
+  // one wave may use up to the CU's 160 KiB of LDS; instance ids fit 8 bits per 64-instance window
+  if (per > 160 * 1024 || ((L.fam[F_COUNT] + 63) / 64) * 64 > 256) return 0;
   return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
 }
 
@@ -1365,13 +1127,13 @@ int expand_blocks_per_cu(const Layout& L) {
     default: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
   }
 
-hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
-                         uint32_t* next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
+hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
+                         const Ring& next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
                          int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags,
                          uint64_t* sent, hipEvent_t mid) {
   if (s_end <= s_begin) return hipSuccess;
   const int cwpb = expand_compact_wpb(L);
-  if (cwpb > 0 && !L.sym && !(xflags & (XF_LANE_KERNEL | XF_WAVE_KERNEL)) && (box.nshard == 1 || sent)) {
+  if (cwpb > 0 && !L.sym && !(xflags & XF_WAVE_KERNEL) && (box.nshard == 1 || sent)) {
     const bool multi = box.nshard > 1;
     {  // k_materialize's range starts at the next-frontier count before this launch
       hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
@@ -1428,52 +1190,14 @@ hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin,
       hipError_t e = hipEventRecord(mid, st);
       if (e != hipSuccess) return e;
     }
-    const size_t mlds = (size_t)cwpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-    RTLA_DISPATCH_N(L, k_materialize, dim3(256 * 16), dim3(64 * cwpb), mlds, st, L, cur, (unsigned long long)cur_base,
+    const size_t mlds = (size_t)lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+    RTLA_DISPATCH_N(L, k_materialize, dim3(256 * 16), dim3(64), mlds, st, L, cur, (unsigned long long)cur_base,
                     next, (const unsigned long long*)parents, (unsigned long long)next_base,
                     (unsigned long long)next_cap, ctr);
     return hipGetLastError();
   }
-  const int wpb = expand_lane_wpb(L);
-  if (wpb > 0 && !L.sym && !(xflags & XF_WAVE_KERNEL)) {  // one lane per state (rows fit LDS)
-    {  // k_materialize's range starts at the next-frontier count before this launch
-      hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
-                                    hipMemcpyDeviceToDevice, st);
-      if (e != hipSuccess) return e;
-    }
-    const uint64_t groups = (s_end - s_begin + 63) / 64;
-    const uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
-    const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-    const bool multi = box.nshard > 1;
-#define RTLA_LANE_CASE(n)                                                                                     \
-  case n: {                                                                                                   \
-    auto kfn = multi ? k_expand_lane<n, true> : k_expand_lane<n, false>;                                      \
-    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)s_begin, \
-                       (unsigned long long)s_end, (unsigned long long)cur_base, next, (unsigned long long*)parents, \
-                       (unsigned long long)next_base, (unsigned long long)next_cap, (unsigned long long*)table,  \
-                       tlog2, ctr, box, xflags);                                                              \
-  } break;
-    switch (L.N) {
-      RTLA_LANE_CASE(1)
-      RTLA_LANE_CASE(2)
-      RTLA_LANE_CASE(3)
-      RTLA_LANE_CASE(4)
-      default: RTLA_LANE_CASE(5)
-    }
-#undef RTLA_LANE_CASE
-    {
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-    if (xflags & XF_NO_MATERIALIZE) return hipSuccess;
-    const int mgrid = 256 * 16;
-    RTLA_DISPATCH_N(L, k_materialize, dim3(mgrid), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)cur_base,
-                    next, (const unsigned long long*)parents, (unsigned long long)next_base,
-                    (unsigned long long)next_cap, ctr);
-    return hipGetLastError();
-  }
-  // one wave per state: rows too wide for 64 per wave in LDS, or SYMMETRY
-  // (the orbit key needs the full Delta of each successor)
+  // one wave per state: SYMMETRY (the orbit key needs the full Delta of each
+  // successor), or rows too wide for the compacting kernel's LDS tile
   RTLA_DISPATCH_N(L, k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
                   (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base, next,
                   (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,
@@ -1496,7 +1220,7 @@ hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts,
   return hipGetLastError();
 }
 
-hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+hipError_t launch_pack_rows(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
                             const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
                             uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, uint64_t max_count,
                             hipStream_t st) {
@@ -1511,7 +1235,7 @@ hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_b
 }
 
 hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, const uint64_t* bases, int nshard,
-                              uint64_t rows_cap, uint32_t* next, uint64_t* parents, uint64_t next_base,
+                              uint64_t rows_cap, const Ring& next, uint64_t* parents, uint64_t next_base,
                               uint64_t next_cap, DevCounters* ctr, uint64_t max_count, hipStream_t st) {
   if (!max_count) return hipSuccess;
   hipLaunchKernelGGL(k_unpack_rows, dim3(grid_x(max_count, 4), nshard), dim3(256), 0, st, W, rows,

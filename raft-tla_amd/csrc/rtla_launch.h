@@ -9,28 +9,27 @@ namespace rtla {
 
 // LDS bytes a k_expand / k_expand_batch block of `wpb` waves needs.
 size_t expand_lds_bytes(const Layout& L, int wpb);
-// Waves per block of the lane-per-state k_expand_lane (0: rows too wide,
-// the wave-per-state k_expand is used).
+// Waves per block of the lane-per-state row builders (k_pack_rows).
 int expand_lane_wpb(const Layout& L);
 // Waves per block of the compacting single-shard kernel (0: not usable).
 int expand_compact_wpb(const Layout& L);
 // Blocks of 4 waves that fit on one CU given the LDS footprint.
 int expand_blocks_per_cu(const Layout& L);
 
-hipError_t launch_expand(const Layout& L, const uint32_t* cur, uint64_t s_begin, uint64_t s_end,
-                         uint64_t cur_base, uint32_t* next, uint64_t* parents, uint64_t next_base,
+hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uint64_t s_end,
+                         uint64_t cur_base, const Ring& next, uint64_t* parents, uint64_t next_base,
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
                          int grid, hipStream_t st, int xflags = 0, uint64_t* sent = nullptr,
                          hipEvent_t mid = nullptr);  // recorded between the probe kernel and k_materialize
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
                                 uint64_t max_count, hipStream_t st);
-hipError_t launch_pack_rows(const Layout& L, const uint32_t* cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+hipError_t launch_pack_rows(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
                             const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
                             uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, uint64_t max_count,
                             hipStream_t st);
 hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, const uint64_t* bases, int nshard,
-                              uint64_t rows_cap, uint32_t* next, uint64_t* parents, uint64_t next_base,
+                              uint64_t rows_cap, const Ring& next, uint64_t* parents, uint64_t next_base,
                               uint64_t next_cap, DevCounters* ctr, uint64_t max_count, hipStream_t st);
 hipError_t launch_part_counts(const uint64_t* new_count, int nshard, uint64_t lo, uint64_t rc, uint64_t* rows_in,
                               uint64_t* bases, DevCounters* ctr, hipStream_t st);

@@ -31,11 +31,17 @@ COVER_NAMES = ["Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientReque
                "HandleAppendEntriesResponse", "DropStaleResponse"]
 
 
+# rtla_level_stats.flags: which capacity ran out (include/rtla.h RTLA_CAP_*)
+CAP_NAMES = {1: "spec-error", 2: "row", 4: "frontier", 8: "fpset", 16: "outbox"}
+
+
 class RtlaError(RuntimeError):
-    def __init__(self, status: int, what: str = ""):
+    def __init__(self, status: int, what: str = "", flags: int = 0):
         self.status = status
+        self.flags = flags
         msg = _lib.rtla_strerror(status).decode() if _lib else str(status)
-        super().__init__("%s: %s (status %d)" % (what, msg, status))
+        caps = [n for b, n in CAP_NAMES.items() if flags & b]
+        super().__init__("%s: %s (status %d%s)" % (what, msg, status, ", " + "+".join(caps) if caps else ""))
 
 
 class _Cfg(C.Structure):
@@ -51,7 +57,8 @@ class _Stats(C.Structure):
                 ("new_states", C.c_uint64), ("generated", C.c_uint64),
                 ("distinct_total", C.c_uint64), ("generated_total", C.c_uint64),
                 ("seconds", C.c_double), ("kernel_ms", C.c_double), ("probes", C.c_uint64),
-                ("row_bytes", C.c_uint64), ("expand_ms", C.c_double)]
+                ("row_bytes", C.c_uint64), ("expand_ms", C.c_double), ("flags", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 def _load():
@@ -301,8 +308,14 @@ class Checker:
         self.status = OK
 
     def step(self) -> int:
+        """One BFS level.  Raises RtlaError (with .flags naming the capacity
+        that ran out) if the level could not be completed."""
         st = _Stats()
-        self.status = _check(_lib.rtla_step(self._h, C.byref(st)), "rtla_step")
+        rc = _lib.rtla_step(self._h, C.byref(st))
+        if rc < 0:
+            self.status = rc
+            raise RtlaError(rc, "rtla_step", st.flags)
+        self.status = rc
         self._rec(st)
         return self.status
 

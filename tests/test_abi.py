@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 def test_python_mirror_binds_every_symbol():
     import rtla
     assert sorted(rtla.EXPORTED) == declared_symbols()
-    assert rtla._lib.rtla_abi_version() == 2
+    assert rtla._lib.rtla_abi_version() == 3
 
 
 def test_row_layout_and_config_errors():
@@ -60,3 +60,13 @@ def test_action_names():
     assert rtla.action_name(cfg, 0, 6) == "Restart(s1)"
     assert rtla.action_name(cfg, 3 + 2, 6) == "Timeout(s3)"
     assert rtla.action_name(cfg, 6 + 1, 6) == "RequestVote(s1, s2)"
+
+
+def test_open_refuses_more_shards_than_the_outbox_holds():
+    """rtla_open checks the shard count before touching a device:
+    more than SHARD_MAX = 8 owners would overflow the kernels' per-owner state."""
+    import rtla
+    for kw in ({"shards": 9}, {"shards": 16}):
+        with pytest.raises(rtla.RtlaError) as e:
+            rtla.Checker(rtla.Config(2, 1, 2, 1, 1, 1, **kw))
+        assert e.value.status == -1

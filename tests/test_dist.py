@@ -27,7 +27,7 @@ def _rank(rank, world, port, out):
     try:
         cid = bench.share_comm_id(rank, lambda: bytes(range(128)))
         t = bench.max_over_ranks(1.0 + rank, world)
-        fpl = bench.fpset_log2_for(bench.DEFAULT, world)
+        fpl = bench.fpset_log2_for(bench.SECONDARY, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -54,13 +54,37 @@ def test_gloo_control_plane(world):
 
 
 def test_fpset_per_rank_sizing():
-    one = bench.fpset_log2_for(bench.DEFAULT, 1)
+    one = bench.fpset_log2_for(bench.SECONDARY, 1)
     assert one == 33
-    distinct = 2_407_297_045  # the default model (tests/golden)
+    distinct = 2_407_297_045  # the exhaust model
     for world in (1, 2, 4, 8):
-        fpl = bench.fpset_log2_for(bench.DEFAULT, world)
+        fpl = bench.fpset_log2_for(bench.SECONDARY, world)
         load = distinct / world / (1 << fpl)
         assert 0.2 < load < 0.3, (world, fpl, load)
         # parent records (0.75 x slots per shard, rtla_host.cpp) hold a shard's states
         assert distinct / world < 0.75 * (1 << fpl)
-    assert bench.fpset_log2_for(bench.DEFAULT, 8, override=28) == 28
+    assert bench.fpset_log2_for(bench.SECONDARY, 8, override=28) == 28
+    # capped workloads keep the one-GPU set per rank (more GPUs reach deeper levels)
+    assert bench.fpset_log2_for("cfg2", 8) == bench.fpset_log2_for("cfg2", 1)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts 2 ranks under
+    torch.distributed.run as a child process; both reach the process group
+    and receive rank 0's id (the GPU work is skipped with --dry-run)."""
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=240,
+                         env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = sorted(l for l in out.stdout.splitlines() if l.startswith("bench.py rank"))
+    assert lines == ["bench.py rank 0 of 2 ready (id 00010203)", "bench.py rank 1 of 2 ready (id 00010203)"], \
+        out.stdout + out.stderr
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

@@ -80,8 +80,6 @@ def test_lockstep_walk_successors_match_oracle(shape):
         mine = sorted((im, rtla.state_text(cfg, r)) for _, _, _, im, r in gpu)
         ref = sorted(walk.successors())
         assert mine == ref, "successor multiset differs at step %d" % step
-        for (_, inst, sub, im, r) in gpu:
-            assert rtla.invariants_violated(cfg, r) == 0 or True
         inm = [x for x in gpu if x[3]]
         if not inm:
             break
@@ -94,17 +92,20 @@ def test_lockstep_walk_successors_match_oracle(shape):
 
 def test_incremental_fingerprint_equals_full_rehash():
     """The kernel derives each successor's fingerprint from its parent's; the
-    materialised row's stored fingerprint must equal a from-scratch hash --
-    checked via the fact that the same state reached by two different paths
-    dedups (counts match golden) and via row identity of repeated states."""
+    stored fingerprint of every successor row (in-model or not) must equal a
+    from-scratch hash of the row, the same state reached along different
+    paths must carry the same fingerprint, and distinct states distinct ones."""
     cfg = rtla.Config(3, 1, 2, 1, 1, 2, ())
     row = rtla.init_row(cfg)
     seen = {}
     frontier = [row]
+    checked = 0
     for _ in range(6):
         succ = rtla.expand_batch(cfg, frontier)
         frontier = []
         for _, _, _, im, r in succ:
+            assert rtla.stored_fingerprint(r) == rtla.row_fingerprint(cfg, r), rtla.state_text(cfg, r)
+            checked += 1
             if not im:
                 continue
             text = rtla.state_text(cfg, r)
@@ -114,6 +115,7 @@ def test_incremental_fingerprint_equals_full_rehash():
             else:
                 seen[text] = fp
                 frontier.append(r)
+    assert checked > 1000
     fps = {}
     for text, fp in seen.items():
         assert fp not in fps, "fingerprint collision between distinct states"
@@ -410,3 +412,61 @@ def test_wave_kernel_without_symmetry_matches_golden():
                                                                    "bfs_counts.json")],
                          env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
+# ---- capacities: the row arena as a ring, overflow is an error, never truncation ----
+def _round64(n):
+    return (n + 63) // 64 * 64
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_ring_arena_wraps_and_matches_golden(shards):
+    """A frontier arena barely larger than the biggest (current + next) level
+    pair: every level wraps around the arena at a different offset; counts and
+    level contents must still be the oracle's."""
+    g = GOLD["n2_v2_t3_l2_m1"]
+    x = [n for n, _ in g["levels"]]
+    # multi-shard: each shard holds about 1/shards of a level (plus skew)
+    need = max(_round64(x[i]) + x[i + 1] for i in range(len(x) - 1))
+    cap = _round64(need // shards + (need // shards) // 4 + 128) if shards > 1 else _round64(need)
+    kw = small_kw(g)
+    kw["mem_budget"] *= shards
+    cfg = cfg_of(g, frontier_cap=cap, shards=shards, chunk=1024, **kw)
+    got = []
+    with rtla.Checker(cfg) as ck:
+        assert '"frontier_cap": %d' % cap in ck.device_info()
+        st = ck.init()
+        while True:
+            rows = ck.frontier()
+            got.append("%016x" % (sum(rv.fnv1a64(rtla.state_text(cfg, r)) for r in rows) & (2**64 - 1)))
+            if st != rtla.OK:
+                break
+            st = ck.step()
+        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
+    assert got[:len(g["level_text_hash"])] == g["level_text_hash"]
+
+
+def test_frontier_overflow_is_an_error():
+    g = GOLD["n2_v2_t3_l2_m1"]
+    cfg = cfg_of(g, frontier_cap=4096, **small_kw(g))
+    with rtla.Checker(cfg) as ck:
+        with pytest.raises(rtla.RtlaError) as e:
+            ck.run()
+        assert e.value.status == -3 and e.value.flags & 4
+        done = [[lv.new, lv.generated] for lv in ck.levels]
+        assert done == g["levels"][:len(done)] and len(done) < len(g["levels"])
+
+
+def test_bag_overflow_is_an_error():
+    """bag_cap = 2 on a model whose states hold 3 distinct messages: the
+    kernel raises RTLA_CAP_ROW (rtla_step -> -3), it never truncates."""
+    g = GOLD["n3_v1_t2_l1_m1"]
+    cfg = rtla.Config(3, 1, 2, 1, 1, 0, ("NoTwoLeaders",), bag_cap=2, fpset_log2=22, mem_budget=1 << 30)
+    with rtla.Checker(cfg) as ck:
+        with pytest.raises(rtla.RtlaError) as e:
+            ck.run()
+        assert e.value.status == -3 and e.value.flags & 2
+    # the oracle agrees that 3 messages are reachable on that model
+    r = raft_cpu.bfs(raft_cpu.cfg_of(3, 1, 2, 1, 1, 0, ("NoTwoLeaders",), max_distinct=100000), threads=4)
+    assert r["max_msgs"] >= 3
+    del g
