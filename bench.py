@@ -145,12 +145,38 @@ def launch_ranks(nproc, argv):
     return subprocess.run(cmd, env=env).returncode
 
 
-def cpu_threads():
-    """Host threads for the CPU baseline: every CPU this process may run on."""
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2
+    cpu.max / v1 cfs quota), or None when unlimited."""
     try:
-        return len(os.sched_getaffinity(0))
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: every CPU this process may run on
+    (affinity), capped by the cgroup's CPU quota -- on the GPU box nproc shows
+    the whole machine but the job gets a share of it; more threads than the
+    share only adds contention."""
+    try:
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cpu_quota()
+    if q:
+        n = min(n, max(1, int(q + 0.999)))
+    return n
 
 
 def cpu_baseline(shape, sample_states, threads):
@@ -161,7 +187,7 @@ def cpu_baseline(shape, sample_states, threads):
     n, v, t, l, c, m, inv = shape
     r = raft_cpu.bfs(raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=sample_states), threads=threads)
     return {"value": r["distinct"] / r["seconds"], "unit": "distinct states/s", "cores": threads,
-            "host_cpus": os.cpu_count(), "kind": "port", "levels": len(r["levels"]),
+            "host_cpus": os.cpu_count(), "cgroup_cpu_quota": cpu_quota(), "kind": "port", "levels": len(r["levels"]),
             "sample": "prefix rate: oracle/raft_cpu.c level-synchronous BFS of the same model, first %d levels "
                       "(%d distinct, %d generated) in %.1f s on %d threads"
                       % (len(r["levels"]), r["distinct"], r["generated"], r["seconds"], threads)}

@@ -10,7 +10,7 @@ namespace rtla {
 // Coverage codes: the 10 Next families, with Receive split into its 6
 // sub-actions (UpdateTerm, HandleRequestVoteRequest, HandleRequestVoteResponse,
 // HandleAppendEntriesRequest, HandleAppendEntriesResponse, DropStaleResponse).
-constexpr int COVER_CODES = F_COUNT + R_NONE;
+constexpr int COVER_CODES = (int)F_COUNT + (int)R_NONE;
 
 enum {
   FLAG_SPEC_ERROR = 1,      // TLC evaluation error (sequence index outside its domain)
@@ -67,7 +67,7 @@ enum {
   XF_NO_PROBE = 1,        // skip the fingerprint-set CAS (every successor "seen")
   XF_NO_COVER = 2,        // skip the coverage counters
   XF_NO_HASH = 4,         // replace the fingerprint delta by a trivial sum
-  XF_NO_MATERIALIZE = 8,  // do not launch k_materialize
+  XF_NO_MATERIALIZE = 8,  // compact kernel: write parent records but not the rows of new states
   XF_NO_CHUNKS = 32,      // compact kernel: load rows + per-state setup only
   XF_NO_DELTA = 64,       // compact kernel: compaction without evaluating actions
   XF_GENERIC_DELTA = 128, // compact kernel: never use the per-family specialised evaluation
@@ -75,6 +75,7 @@ enum {
   XF_NO_PERSIST = 512,    // compact kernel: one group per wave instead of persistent waves
   XF_CAS_ONLY = 1024,     // compact kernel: probe with CAS only (no load-first)
   XF_WAVE_KERNEL = 2048,  // use the wave-per-state k_expand (the SYMMETRY path) without symmetry
+  XF_NO_SPECIAL = 4096,   // compact kernel: run-time layout even for a compiled-in configuration
 };
 
 // Per-level device counters (zeroed before each level except `cover`).
@@ -88,7 +89,7 @@ struct DevCounters {
   int viol_in_model;
   unsigned long long viol_parent;
   unsigned long long viol_child;
-  unsigned long long mat_begin;  // k_materialize: first next-frontier slot of the current expand launch
+  unsigned long long group_next;  // k_expand_compact's work queue (zeroed before each launch)
   // buffer capacities (rows of the current / next frontier, parent records), for RTLA_CHECKED builds
   unsigned long long cap_cur, cap_next, cap_parents;
   unsigned long long cover[2 * COVER_CODES];  // [0,C): generated, [C,2C): distinct

@@ -496,7 +496,7 @@ static int env_xflags() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RTLA_XFLAGS");
-    v = e ? (atoi(e) & (XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL)) : 0;
+    v = e ? (atoi(e) & (XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL | XF_NO_SPECIAL)) : 0;
   }
   return v;
 }
@@ -889,7 +889,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
     uint64_t blocks = (s.n_cur + 3) / 4;
     int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
-    HIPCHK(hipEventRecord(s.evm, x->stream));  // (re-recorded between the kernels when k_materialize runs)
+    HIPCHK(hipEventRecord(s.evm, x->stream));  // (re-recorded after the level kernel)
     HIPCHK(launch_expand(L, cur_ring(x, s), 0, s.n_cur, s.cur_base, next_ring(x, s), s.parents, next_base[0],
                          next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), nullptr, s.evm));
   } else {

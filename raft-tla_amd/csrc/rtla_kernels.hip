@@ -268,7 +268,7 @@ k_expand(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_en
     const int ncand = fixed + 3 * nmsg;
     for (int base = 0; base < ncand; base += 64) {
       const int q = base + lane;
-      Delta d;
+      DeltaT<NS> d;
       d.enabled = 0;
       int inst = 0;
       if (q < ncand) {
@@ -369,12 +369,17 @@ k_expand(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_en
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
 }
 
-// Helpers of the lane-per-state phases (k_expand_compact, k_materialize, k_pack_rows).
+// Helpers of the lane-per-state phases (k_expand_compact, k_pack_rows).
 namespace {
 
 struct LaneWords {  // word w of a per-lane array kept word-major (stride 64: bank-conflict free)
   uint32_t* p;
   __device__ __forceinline__ uint32_t& operator[](int w) const { return p[w * 64]; }
+};
+template <int S>
+struct StridedWords {  // the same with stride S (one array per state of an S-state group)
+  uint32_t* p;
+  __device__ __forceinline__ uint32_t& operator[](int w) const { return p[w * S]; }
 };
 
 __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
@@ -410,8 +415,12 @@ constexpr int NEWCAP = 128; // new-state list (u64 parent records)
 
 constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
 
-__host__ __device__ constexpr int compact_lds_words(int W, int AW) {
-  return 64 * W + 64 * AW + RING / 2 + 2 * NEWCAP + 4 * SHARD_MAX;  // + per-owner (base, used) of the open outbox chunk
+// Per-wave LDS of k_expand_compact (16-byte aligned pieces first):
+// per-state fingerprint with allLogs' applied (GROUP FPs) | per-owner (base,
+// used) of the open outbox chunk | pending new states (NEWCAP parent records)
+// | GROUP rows | allLogs' words of each state | pair ring.
+__host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP) {
+  return (4 * GROUP + 4 * SHARD_MAX + 2 * NEWCAP + GROUP * W + GROUP * AW + RING / 2 + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -482,23 +491,38 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #ifndef RTLA_COMPACT_WAVES_PER_EU
 #define RTLA_COMPACT_WAVES_PER_EU 3  // 166 VGPRs for N = 3 without spills (the default allocation took 170 -> 2 waves)
 #endif
-template <int NS, bool MULTI>
+// The layout the kernel runs on: the run-time argument, or (LC.N != 0) the
+// configuration compiled in as a template parameter, whose fields the
+// compiler then folds into every offset, bound and loop of the model code.
+template <Layout LC>
+__device__ __forceinline__ const Layout& pick_layout(const Layout& rt) {
+  if constexpr (LC.N == 0) return rt;
+  else return LC;
+}
+
+// GROUP: frontier states per wave-group (64, or 32 for wide rows: halves the
+// LDS tile so more waves fit a CU).  LC: compiled-in layout (Layout{} = use
+// the run-time argument Lrt).
+template <int NS, bool MULTI, int GROUP, Layout LC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_COMPACT_WAVES_PER_EU)))
-k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_end,
-                 unsigned long long cur_base, unsigned long long* __restrict__ parents, unsigned long long next_base,
-                 unsigned long long next_cap, unsigned long long* table, unsigned long long* sent, int tlog2,
-                 DevCounters* ctr, ShardBox box, int xflags) {
+k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long long s_end,
+                 unsigned long long cur_base, Ring next, unsigned long long* __restrict__ parents,
+                 unsigned long long next_base, unsigned long long next_cap, unsigned long long* table,
+                 unsigned long long* sent, int tlog2, DevCounters* ctr, ShardBox box, int xflags) {
+  const Layout& L = pick_layout<LC>(Lrt);
   const int me = box.me;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wpb = blockDim.x >> 6;
   const int W = L.W, AW = L.all_words;
-  uint32_t* rows = lds + wave * compact_lds_words(W, AW);
-  const LaneWords pall_mine{rows + 64 * W + lane};
-  uint16_t* ring = reinterpret_cast<uint16_t*>(rows + 64 * W + 64 * AW);
-  unsigned long long* newl = reinterpret_cast<unsigned long long*>(rows + 64 * W + 64 * AW + RING / 2);
-  unsigned long long* obox = newl + NEWCAP;  // [o] = base of the open chunk, [SHARD_MAX + o] = slots used
+  uint32_t* wl = lds + wave * compact_lds_words(W, AW, GROUP);
+  FP* pfpl = reinterpret_cast<FP*>(wl);  // [state lane]: its fingerprint + the allLogs' change (raft.tla:465)
+  unsigned long long* obox = reinterpret_cast<unsigned long long*>(wl + 4 * GROUP);  // [o] base of the open chunk, [SHARD_MAX + o] used
+  unsigned long long* newl = obox + 2 * SHARD_MAX;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(newl + NEWCAP);
+  uint32_t* pall = rows + GROUP * W;  // allLogs' words of state lane l: pall[l + w * GROUP]
+  const StridedWords<GROUP> pall_mine{pall + (lane & (GROUP - 1))};
+  uint16_t* ring = reinterpret_cast<uint16_t*>(pall + GROUP * AW);
   if (MULTI) {
     if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
@@ -517,30 +541,121 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
   // first time this shard meets it, its (fingerprint, parent) record goes to
   // the owner's outbox; later copies are dropped (the owner already has it).
   bool pend = false;
-  unsigned long long pold = 0, pidx = 0, prec = 0;
-  FP pf{0, 0};
-  int powner = 0;
-  int nnew = 0;  // entries in newl (uniform)
+  unsigned long long pold = 0;
+  FP pf{0, 0};       // its fingerprint (home slot and owner derive from it)
+  uint32_t pinfo = 0;  // its state lane << 16 | action instance
+  // New states found so far whose rows are not built yet: newl[head, tail)
+  // (mod NEWCAP) holds their parent records; their parents are rows of the
+  // current group (uniform counters).
+  int head = 0, tail = 0;
+  unsigned long long s0 = 0;  // first state of the current group
+#ifdef RTLA_PFP_SHFL
+  FP pfp0{0, 0}, pfp{0, 0};
+#endif
 
-  auto flush_new = [&]() {
-    // reserve nnew slots with one atomic, then write the parent records
-    unsigned long long obase = 0;
-    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)nnew);
-    obase = shfl0_u64(obase);
-    // Slots past next_cap are dropped (and flagged); the ones below it are
-    // always written, so k_materialize never reads an unwritten record.
-    if (obase + nnew > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
-    for (int k = lane; k < nnew; k += 64)
-      if (obase + k < next_cap && RTLA_IDX_OK(ctr, next_base + obase + k, ctr->cap_parents))
-        parents[next_base + obase + k] = newl[k];
-    wave_sync();
-    nnew = 0;
+  // One atomic reserves nb next-level slots.  Slots past next_cap are
+  // dropped and flagged (the level is then reported incomplete).
+  auto reserve = [&](int nb) {
+    unsigned long long ob = 0;
+    if (lane == 0) ob = atomicAdd(&ctr->next_count, (unsigned long long)nb);
+    ob = shfl0_u64(ob);
+    if (ob + nb > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    return ob;
+  };
+  // Build the rows of the nb oldest pending new states into slots obase ..
+  // obase + nb - 1 of the next level, one state per lane:
+  //  (1) the wave copies each parent row (LDS) to its child's slot with
+  //      coalesced stores;
+  //  (2) each lane re-derives its successor's full Delta (compute_delta with
+  //      slot bookkeeping; the probe pass only folded it into a hash), its
+  //      fingerprint, invariants and distinct coverage -- arithmetic that
+  //      overlaps the stores and the chunk's probe loads in flight;
+  //  (3) after the stores completed, each lane stores the words in which its
+  //      child differs from the parent (child_patches, rtla_model.h).
+  // This replaces a separate row-building kernel: no parent-record read, no
+  // parent-row gather, no second launch.
+  auto build_rows = [&](unsigned long long obase, int nb) {
+    const bool act = lane < nb;
+    const unsigned long long pr = act ? newl[(head + lane) & (NEWCAP - 1)] : 0ull;
+    const int sl = act ? (int)(((pr >> 16) & ((1ull << 40) - 1ull)) - (cur_base + s0)) : 0;
+    const int inst = (int)(pr & 0xffffull);
+    const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nb, next_cap - obase);
+    const bool rows_on = !(xflags & XF_NO_MATERIALIZE) && RTLA_IDX_OK(ctr, obase + nrows, ctr->cap_next + 1);
+    const unsigned long long p0 = ring_idx(next, obase);
+    const int n1 = (int)min<unsigned long long>(next.cap - p0, (unsigned long long)nrows) * W;  // words before the wrap
+    uint32_t* d1 = next.base + p0 * (unsigned long long)W;
+    if (rows_on) {  // (1)
+      const int nwords = nrows * W;
+      int r = 0, w = lane;
+      while (w >= W) { w -= W; r++; }
+      for (int i0 = 0; i0 < nwords; i0 += 64) {
+        const int sr = __shfl(sl, r & 63);
+        const int i = i0 + lane;
+        if (i < nwords) {
+          const uint32_t v = rows[sr * W + w];
+          if (i < n1) d1[i] = v;
+          else next.base[i - n1] = v;
+        }
+        w += 64;
+        while (w >= W) { w -= W; r++; }
+      }
+    }
+    DeltaT<NS> d;  // (2)
+    d.enabled = 0;
+    if (act) compute_delta<NS>(L, rows + sl * W, inst, d);
+#ifdef RTLA_PFP_SHFL
+    const FP qfp{shfl_u64(pfp.a, sl), shfl_u64(pfp.b, sl)};
+#else
+    const FP qfp = pfpl[sl];
+#endif
+    FP cfp{0, 0};
+    if (act) {
+      const uint32_t* prow = rows + sl * W;
+      cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
+      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+      if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+        ctr->viol_parent = cur_base + s0 + sl;
+        ctr->viol_inst = inst;
+        ctr->viol_in_model = 1;
+        ctr->viol_child = lane < nrows ? next_base + obase + lane : ~0ull;
+      }
+    }
+    if (!(xflags & XF_NO_COVER)) {  // distinct coverage, aggregated over equal codes
+      const int code = act ? cover_code(L, inst, d.sub) : -1;
+      const unsigned long long am = __ballot(act);
+      if (am) {
+        const int c0 = __shfl(code, __builtin_ctzll(am));
+        const bool same = act && code == c0;
+        const int n0 = __popcll(__ballot(same));
+        if (lane == 0) atomicAdd(&cov[COVER_CODES + c0], (unsigned)n0);
+        if (act && !same) atomicAdd(&cov[COVER_CODES + code], 1u);
+      }
+    }
+    if (rows_on) {  // (3): the copies must land first (same words, other lanes)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < nrows) {
+        const StridedWords<GROUP> pall_p{pall + sl};
+        const int off = lane * W;
+        child_patches<NS>(L, rows + sl * W, d, pall_p, cfp, [&](int w, uint32_t v) {
+          const int i = off + w;
+          if (i < n1) d1[i] = v;
+          else next.base[i - n1] = v;
+        });
+      }
+    }
+    if (lane < nrows && RTLA_IDX_OK(ctr, next_base + obase + lane, ctr->cap_parents))
+      parents[next_base + obase + lane] = pr;
+    head += nb;
   };
   auto resolve = [&]() {
     bool isnew = false;
+    const int powner = MULTI ? fp_owner(pf, box.nshard) : me;
+    const unsigned long long prec =
+        (unsigned long long)me << 56 | (cur_base + s0 + (pinfo >> 16)) << 16 | (unsigned long long)(pinfo & 0xffffu);
     if (pend) {
       const bool to_sent = MULTI && powner != me;
       unsigned long long* t = to_sent ? sent : table;
+      const unsigned long long pidx = pf.a >> (64 - tlog2);
       isnew = (xflags & XF_CAS_ONLY) ? fpset_resolve(t, tlog2, pf.b | 1ull, pidx, pold, ctr)
                                      : fpset_resolve_loaded(t, tlog2, pf.b | 1ull, pidx, pold, ctr, to_sent);
     }
@@ -582,32 +697,45 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
     }
     const unsigned long long m = __ballot(isnew);
     if (m) {
-      if (isnew) newl[nnew + __popcll(m & lanes_below)] = prec;
-      nnew += __popcll(m);
+      if (isnew) newl[(tail + __popcll(m & lanes_below)) & (NEWCAP - 1)] = prec;
+      tail += __popcll(m);
       wave_sync();
-      if (nnew >= 64) flush_new();
     }
     pend = false;
   };
 
-  for (unsigned long long s0 = s_begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; s0 < s_end;
-       s0 += (unsigned long long)gridDim.x * wpb * 64ull) {
-    const int nvalid = (int)min<unsigned long long>(64ull, s_end - s0);
-    {  // s0 and cur.start are multiples of 64: the group's rows are contiguous in the arena
+  // Groups are handed out by a device-wide counter (one atomic per group,
+  // the next one requested while the current group is processed): a wave
+  // that became resident late, or drew heavy groups, simply takes fewer --
+  // no static partition, no tail.  (The occupancy API can over-report the
+  // resident blocks by one per CU; a static stride would then serialise 1/k
+  // of the work behind the rest.)
+  const unsigned long long ngroups = (s_end - s_begin + GROUP - 1) / GROUP;
+  unsigned long long gnext = 0;
+  if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
+  for (unsigned long long gi = shfl0_u64(gnext); gi < ngroups; gi = shfl0_u64(gnext)) {
+    if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
+    s0 = s_begin + gi * GROUP;
+    const int nvalid = (int)min<unsigned long long>((unsigned long long)GROUP, s_end - s0);
+    {  // s0 and cur.start are multiples of GROUP: the group's rows are contiguous in the arena
       const uint32_t* src = ring_row(cur, s0, W);
       const int nw = nvalid * W;
       if (RTLA_IDX_OK(ctr, ring_idx(cur, s0) + nvalid, cur.cap + 1)) copy_words_lds(rows, src, nw, lane);
     }
     wave_sync();
     const bool valid = lane < nvalid;
-    const uint32_t* prow_mine = rows + lane * W;
-    FP pfp0{0, 0}, pfp{0, 0};
+    const uint32_t* prow_mine = rows + (lane & (GROUP - 1)) * W;
     int nmsg = 0;
     if (valid) {
+#ifdef RTLA_PFP_SHFL
       pfp0 = row_fp(prow_mine);
       pfp = fp_add(pfp0, alllogs_delta<NS>(L, prow_mine, pall_mine));
+#else
+      pfpl[lane] = fp_add(row_fp(prow_mine), alllogs_delta<NS>(L, prow_mine, pall_mine));
+#endif
       nmsg = row_nmsg(L, prow_mine);
     }
+    wave_sync();
     for (int wb = 0; wb < ((xflags & XF_NO_CHUNKS) ? 0 : ninst); wb += 64) {
       const unsigned long long mask = valid ? cand_mask<NS>(L, prow_mine, nmsg, wb) : 0ull;
       unsigned long long todo = wave_or_u64(mask);
@@ -646,9 +774,13 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
         const int e = active ? ring[(done + lane) & (RING - 1)] : 0;
         const int sl = e >> 8, inst = wb + (e & 255);
         const uint32_t* prow = rows + sl * W;
+#ifdef RTLA_PFP_SHFL
         const FP qfp{shfl_u64(pfp.a, sl), shfl_u64(pfp.b, sl)};
         const FP qfp0{shfl_u64(pfp0.a, sl), shfl_u64(pfp0.b, sl)};
-        DeltaFp d;
+#else
+        const FP qfp = pfpl[sl];
+#endif
+        DeltaFpT<NS> d;
         d.enabled = 0;
         if (!(xflags & XF_NO_DELTA)) {
           const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
@@ -683,6 +815,9 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
         if (en && d.in_model) {
           const FP cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
                                                 : fp_add(qfp, delta_fp<NS>(L, prow, d));
+#ifndef RTLA_PFP_SHFL
+          const FP qfp0 = row_fp(prow);
+#endif
           if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
             probe = !(xflags & XF_NO_PROBE);
             cf = cfp;
@@ -710,14 +845,19 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
             ctr->viol_child = ~0ull;
           }
         }
-        resolve();  // the previous chunk's CAS, after this chunk's arithmetic
+        resolve();  // the previous chunk's probes, after this chunk's arithmetic
+        // 64 new states pending: reserve their slots now (the returning
+        // atomic waits only for itself: every older load has been consumed),
+        // build their rows after this chunk's probes are issued
+        const bool flush = tail - head >= 64;
+        unsigned long long fbase = 0;
+        if (flush) fbase = reserve(64);
+        asm volatile("" ::: "memory");
         if (probe) {
           my_probe++;
           pend = true;
           pf = cf;
-          pidx = idx;
-          powner = owner;
-          prec = (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
+          pinfo = (uint32_t)sl << 16 | (uint32_t)inst;
           unsigned long long* slotp = &((MULTI && owner != me) ? sent : table)[idx];
           // load first: most successors are already in the set, and a plain
           // load is cheaper than an atomic at the memory side; the CAS is
@@ -725,13 +865,19 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
           pold = (xflags & XF_CAS_ONLY) ? atomicCAS(slotp, 0ull, cf.b | 1ull)
                                         : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (flush) build_rows(fbase, 64);
         done += cnt;
       }
     }
-    wave_sync();  // the next group overwrites this group's rows
+    // Group end: the last probes and every pending row (their parents are
+    // this group's rows, which the next group overwrites).
+    resolve();
+    while (tail > head) {
+      const int nb = min(64, tail - head);
+      build_rows(reserve(nb), nb);
+    }
+    wave_sync();
   }
-  resolve();
-  if (nnew) flush_new();
   if (MULTI) {
     for (int o = 0; o < box.nshard; o++) {
       const unsigned long long b = obox[o], used = obox[SHARD_MAX + o];
@@ -745,71 +891,8 @@ k_expand_compact(Layout L, Ring cur, unsigned long long s_begin, unsigned long l
   if (lane == 0 && my_gen) atomicAdd(&ctr->generated, (unsigned long long)my_gen);
   if (lane == 0 && my_probe) atomicAdd(&ctr->probes, (unsigned long long)my_probe);
   __syncthreads();
-  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
+  for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x)
     if (cov[k]) atomicAdd(&ctr->cover[k], (unsigned long long)cov[k]);
-}
-
-// k_materialize: build the rows of the new states k_expand_compact found.
-// Slots [ctr->mat_begin, ctr->next_count) of the next frontier hold only a
-// parent record (shard << 56 | parent index << 16 | action instance); one
-// lane per slot stages its parent row in LDS, re-derives the successor with
-// the full Delta, writes the row with its fingerprint, checks the invariants
-// (raft.cfg:3, specs/MC.tla) and counts the distinct coverage.
-template <int NS>
-__global__ void __launch_bounds__(256)
-k_materialize(Layout L, Ring cur, unsigned long long cur_base, Ring next,
-              const unsigned long long* __restrict__ parents, unsigned long long next_base,
-              unsigned long long next_cap, DevCounters* ctr) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ unsigned int cov[COVER_CODES];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wpb = blockDim.x >> 6;
-  const int W = L.W, AW = L.all_words;
-  uint32_t* rows = lds + wave * lane_lds_words(W, AW);
-  uint32_t* prow = rows + lane * W;
-  const LaneWords pall{rows + 64 * W + lane};
-  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
-  __syncthreads();
-  const unsigned long long begin = ctr->mat_begin;
-  const unsigned long long end = min(ctr->next_count, next_cap);
-  for (unsigned long long g = begin + ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; g < end;
-       g += (unsigned long long)gridDim.x * wpb * 64ull) {
-    const int nv = (int)min<unsigned long long>(64ull, end - g);
-    const unsigned long long slot = g + lane;
-    const bool act = lane < nv;
-    const unsigned long long pr =
-        act && RTLA_IDX_OK(ctr, next_base + slot, ctr->cap_parents) ? parents[next_base + slot] : 0ull;
-    const unsigned long long sidx = ((pr >> 16) & ((1ull << 40) - 1ull)) - cur_base;
-    const int inst = (int)(pr & 0xffffull);
-    // gather the parent rows: one coalesced row read per slot (rows stay in L2)
-    gather_rows_lds(rows, W, nv, [&](int r) {
-      const unsigned long long sr = readlane_u64(sidx, r);
-      return ring_row(cur, RTLA_IDX_OK(ctr, sr, ctr->cap_cur) ? sr : 0ull, W);
-    }, lane);
-    wave_sync();
-    if (act) {
-      const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
-      Delta d;
-      compute_delta<NS>(L, prow, inst, d);
-      const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
-      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-      if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-        ctr->viol_parent = sidx + cur_base;
-        ctr->viol_inst = inst;
-        ctr->viol_in_model = 1;
-        ctr->viol_child = next_base + slot;
-      }
-      atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
-      materialize<NS>(L, prow, d, pall, cfp, prow);  // in place: the parent row is not read again
-    }
-    wave_sync();
-    // the group's rows are consecutive states of the next level: coalesced stores
-    if (RTLA_IDX_OK(ctr, g + nv, ctr->cap_next + 1)) store_rows_ring(next, g, nv, W, rows, lane);
-    wave_sync();
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
-    if (cov[k]) atomicAdd(&ctr->cover[COVER_CODES + k], (unsigned long long)cov[k]);
 }
 
 // Owner side of the exchange: insert the fingerprints other shards sent and
@@ -912,7 +995,7 @@ k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
     uint32_t* prow = lrows + lane * W;
     if (act) {
       const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
-      Delta d;
+      DeltaT<NS> d;
       compute_delta<NS>(L, prow, inst, d);
       const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
       const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
@@ -1021,7 +1104,7 @@ k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n
     const int ncand = fixed + 3 * nmsg;
     for (int base = 0; base < ncand; base += 64) {
       const int q = base + lane;
-      Delta d;
+      DeltaT<NS> d;
       d.enabled = 0;
       int inst = 0;
       if (q < ncand) {
@@ -1094,6 +1177,15 @@ int expand_lane_wpb(const Layout& L) {
   return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
 }
 
+// States per wave-group of k_expand_compact: 64, or 32 when 64 rows would
+// make the per-wave LDS tile so large that fewer than ~11 waves fit a CU.
+#ifndef RTLA_GROUP64_LDS
+#define RTLA_GROUP64_LDS (16 * 1024)
+#endif
+constexpr int compact_group(const Layout& L) {
+  return compact_lds_words(L.W, L.all_words, 64) * sizeof(uint32_t) <= RTLA_GROUP64_LDS ? 64 : 32;
+}
+
 static int device_cus() {
   static int cus = 0;
   if (!cus) {
@@ -1105,8 +1197,9 @@ static int device_cus() {
   return cus;
 }
 
+
 int expand_compact_wpb(const Layout& L) {
-  const size_t per = (size_t)compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+  const size_t per = (size_t)compact_lds_words(L.W, L.all_words, compact_group(L)) * sizeof(uint32_t);
   // one wave may use up to the CU's 160 KiB of LDS; instance ids fit 8 bits per 64-instance window
   if (per > 160 * 1024 || ((L.fam[F_COUNT] + 63) / 64) * 64 > 256) return 0;
   return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
@@ -1127,6 +1220,45 @@ int expand_blocks_per_cu(const Layout& L) {
     default: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
   }
 
+// Configurations whose layout is compiled into k_expand_compact (the BASELINE
+// workloads bench.py runs); any other configuration runs the same kernel on
+// its run-time layout.
+namespace specs {
+constexpr Layout CFG2 = layout_of(3, 2, 3, 2, 1, 0, 18, 6, INV_ELECTION_SAFETY | INV_LOG_MATCHING);  // configs[1]
+constexpr Layout CFG1 = layout_of(3, 1, 2, 1, 1, 0, 24, 3, INV_NO_TWO_LEADERS);                     // configs[0]
+constexpr Layout EXHAUST = layout_of(3, 2, 2, 2, 1, 2, 3, 3, INV_ELECTION_SAFETY | INV_LOG_MATCHING);
+static_assert(CFG2.N == 3 && CFG1.N == 3 && EXHAUST.N == 3, "compiled-in layouts must be valid");
+}  // namespace specs
+
+template <int NS, int GROUP, Layout LC>
+static hipError_t launch_compact(const Layout& L, bool multi, const Ring& cur, uint64_t s_begin, uint64_t s_end,
+                                 uint64_t cur_base, const Ring& next, uint64_t* parents, uint64_t next_base,
+                                 uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
+                                 hipStream_t st, int xflags, uint64_t* sent, int wpb) {
+  auto kfn = multi ? k_expand_compact<NS, true, GROUP, LC> : k_expand_compact<NS, false, GROUP, LC>;
+  const uint64_t groups = (s_end - s_begin + GROUP - 1) / GROUP;
+  uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
+  const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words, GROUP) * sizeof(uint32_t);
+  if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
+    static int per_cu[2][2];  // per instantiation: [multi][one-wave blocks]
+    int& pc = per_cu[multi][wpb == 1];
+    if (!pc) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kfn, 64 * wpb, lds) != hipSuccess || pc < 1)
+        pc = 16 / wpb;
+    }
+    blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * pc);
+  }
+  {
+    hipError_t e = hipMemsetAsync(&ctr->group_next, 0, sizeof(ctr->group_next), st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)s_begin,
+                     (unsigned long long)s_end, (unsigned long long)cur_base, next, (unsigned long long*)parents,
+                     (unsigned long long)next_base, (unsigned long long)next_cap, (unsigned long long*)table,
+                     (unsigned long long*)sent, tlog2, ctr, box, xflags);
+  return hipGetLastError();
+}
+
 hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
                          const Ring& next, uint64_t* parents, uint64_t next_base, uint64_t next_cap, uint64_t* table,
                          int tlog2, DevCounters* ctr, const ShardBox& box, int grid, hipStream_t st, int xflags,
@@ -1135,65 +1267,41 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
   const int cwpb = expand_compact_wpb(L);
   if (cwpb > 0 && !L.sym && !(xflags & XF_WAVE_KERNEL) && (box.nshard == 1 || sent)) {
     const bool multi = box.nshard > 1;
-    {  // k_materialize's range starts at the next-frontier count before this launch
-      hipError_t e = hipMemcpyAsync(&ctr->mat_begin, &ctr->next_count, sizeof(unsigned long long),
-                                    hipMemcpyDeviceToDevice, st);
-      if (e != hipSuccess) return e;
-    }
     const int wpb = (xflags & XF_BLOCK4) ? cwpb : 1;  // one-wave workgroups by default
-    const uint64_t groups = (s_end - s_begin + 63) / 64;
-    uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
-    if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
-      static int per_cu[2][2][NMAX + 1];
-      int& pc = per_cu[multi][wpb == 1][L.N];
-      if (!pc) {
-        const size_t l = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-        hipError_t e = hipErrorInvalidValue;
-#define RTLA_OCC(n) \
-  e = multi ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<n, true>, 64 * wpb, l) \
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k_expand_compact<n, false>, 64 * wpb, l)
-        switch (L.N) {
-          case 1: RTLA_OCC(1); break;
-          case 2: RTLA_OCC(2); break;
-          case 3: RTLA_OCC(3); break;
-          case 4: RTLA_OCC(4); break;
-          default: RTLA_OCC(5); break;
-        }
-#undef RTLA_OCC
-        if (e != hipSuccess || pc < 1) pc = 16 / wpb;
+    hipError_t e = hipSuccess;
+#define RTLA_ARGS L, multi, cur, s_begin, s_end, cur_base, next, parents, next_base, next_cap, table, tlog2, ctr, box, \
+                  st, xflags, sent, wpb
+#define RTLA_SPEC(S)                                                                               \
+  if (!done && same_layout(L, specs::S)) {                                                         \
+    e = launch_compact<specs::S.N, compact_group(specs::S), specs::S>(RTLA_ARGS);                  \
+    done = true;                                                                                   \
+  }
+    bool done = false;
+    if (!(xflags & XF_NO_SPECIAL)) {
+      RTLA_SPEC(CFG2)
+      RTLA_SPEC(CFG1)
+      RTLA_SPEC(EXHAUST)
+    }
+    if (!done) {  // run-time layout
+      const bool g64 = compact_group(L) == 64;
+#define RTLA_GENERIC(n) \
+  case n: e = g64 ? launch_compact<n, 64, Layout{}>(RTLA_ARGS) : launch_compact<n, 32, Layout{}>(RTLA_ARGS); break;
+      switch (L.N) {
+        RTLA_GENERIC(1)
+        RTLA_GENERIC(2)
+        RTLA_GENERIC(3)
+        RTLA_GENERIC(4)
+        default: RTLA_GENERIC(5)
       }
-      blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * pc);
+#undef RTLA_GENERIC
     }
-    const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-#define RTLA_COMPACT_CASE(n)                                                                                \
-  case n: {                                                                                                 \
-    auto kfn = multi ? k_expand_compact<n, true> : k_expand_compact<n, false>;                              \
-    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, L, cur, (unsigned long long)s_begin, \
-                       (unsigned long long)s_end, (unsigned long long)cur_base, (unsigned long long*)parents,  \
-                       (unsigned long long)next_base, (unsigned long long)next_cap, (unsigned long long*)table, \
-                       (unsigned long long*)sent, tlog2, ctr, box, xflags);                                   \
-  } break;
-    switch (L.N) {
-      RTLA_COMPACT_CASE(1)
-      RTLA_COMPACT_CASE(2)
-      RTLA_COMPACT_CASE(3)
-      RTLA_COMPACT_CASE(4)
-      default: RTLA_COMPACT_CASE(5)
-    }
-#undef RTLA_COMPACT_CASE
-    {
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-    if (xflags & XF_NO_MATERIALIZE) return hipSuccess;
+#undef RTLA_SPEC
+#undef RTLA_ARGS
+    if (e != hipSuccess) return e;
     if (mid) {
-      hipError_t e = hipEventRecord(mid, st);
+      e = hipEventRecord(mid, st);
       if (e != hipSuccess) return e;
     }
-    const size_t mlds = (size_t)lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-    RTLA_DISPATCH_N(L, k_materialize, dim3(256 * 16), dim3(64), mlds, st, L, cur, (unsigned long long)cur_base,
-                    next, (const unsigned long long*)parents, (unsigned long long)next_base,
-                    (unsigned long long)next_cap, ctr);
     return hipGetLastError();
   }
   // one wave per state: SYMMETRY (the orbit key needs the full Delta of each

@@ -11,7 +11,7 @@ namespace rtla {
 size_t expand_lds_bytes(const Layout& L, int wpb);
 // Waves per block of the lane-per-state row builders (k_pack_rows).
 int expand_lane_wpb(const Layout& L);
-// Waves per block of the compacting single-shard kernel (0: not usable).
+// Waves per block of the compacting level kernel (0: not usable).
 int expand_compact_wpb(const Layout& L);
 // Blocks of 4 waves that fit on one CU given the LDS footprint.
 int expand_blocks_per_cu(const Layout& L);
@@ -20,7 +20,7 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
                          uint64_t cur_base, const Ring& next, uint64_t* parents, uint64_t next_base,
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
                          int grid, hipStream_t st, int xflags = 0, uint64_t* sent = nullptr,
-                         hipEvent_t mid = nullptr);  // recorded between the probe kernel and k_materialize
+                         hipEvent_t mid = nullptr);  // recorded after the level kernel
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
                                 uint64_t max_count, hipStream_t st);

@@ -46,6 +46,7 @@
 // ---------------------------------------------------------------------------
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
@@ -83,6 +84,11 @@ enum {
 // Invariant bits (build-defined model wrapper, oracle/MC.tla).
 enum { INV_NO_TWO_LEADERS = 1, INV_ELECTION_SAFETY = 2, INV_LOG_MATCHING = 4 };
 
+// A model's row format.  Plain ints only (a C++20 structural type): the
+// kernels take it either as a run-time argument or, for the configurations
+// compiled in ahead of time (rtla_kernels.hip, LayoutSpecs), as a template
+// parameter -- then every offset, bound and family range below is a
+// compile-time constant in the generated code.
 struct Layout {
   int N, V, T, L, C, M, K, E;
   int inv_mask;
@@ -95,8 +101,7 @@ struct Layout {
 };
 
 // Returns 0 on success, <0 if the configuration exceeds the row format.
-static inline int make_layout(Layout* l, int N, int V, int T, int L, int C, int M, int K, int E,
-                              int inv_mask) {
+constexpr int make_layout(Layout* l, int N, int V, int T, int L, int C, int M, int K, int E, int inv_mask) {
   if (N < 1 || N > NMAX || V < 1 || V > VMAX || T < 1 || T > TMAX || L < 0 || L > LMAX ||
       C < 1 || C > CMAX || M < 0 || K < 1 || K > KMAX || E < 0 || E > EMAX)
     return -1;
@@ -133,6 +138,13 @@ static inline int make_layout(Layout* l, int N, int V, int T, int L, int C, int 
   l->fam[F_COUNT] = f;
   return 0;
 }
+// The same by value (N = 0 on a configuration outside the row format).
+constexpr Layout layout_of(int N, int V, int T, int L, int C, int M, int K, int E, int inv_mask) {
+  Layout l{};
+  if (make_layout(&l, N, V, T, L, C, M, K, E, inv_mask) != 0) return Layout{};
+  return l;
+}
+static inline bool same_layout(const Layout& a, const Layout& b) { return memcmp(&a, &b, sizeof(Layout)) == 0; }
 
 // Run-time-indexed reads of the Layout tables as select chains: on the GPU a
 // dynamically indexed kernel-argument array becomes a vector memory load, and
@@ -351,20 +363,23 @@ RTLA_HD void row_init(const Layout& L, P row) {
 // fixed the loops over servers unroll and every array in Delta is indexed
 // with compile-time constants, so the whole Delta stays in VGPRs on the GPU
 // (no scratch); writes at a run-time index go through set_at().
-struct Delta {
+// NR: servers the record arrays are sized for (NS in the kernels, NMAX on the host).
+template <int NR = NMAX>
+struct DeltaT {
   int32_t enabled;
   int32_t in_model;
   int32_t sub;             // Receive sub-action (R_*) or R_NONE
   int32_t err;             // 1: spec evaluation error, 2: row capacity overflow
   int32_t srv;             // server whose record changes, -1 = none
-  uint32_t rec[3 + NMAX];  // its new record
+  uint32_t rec[3 + NR];    // its new record
   int32_t nops;            // bag slot writes (<= 3)
   int32_t op_slot[3];
   uint64_t op_old[3], op_new[3];
   int32_t nmsg;            // new number of bag slots in use
   int32_t elec;            // 1: append erec to elections
-  uint32_t erec[2 + NMAX];
+  uint32_t erec[2 + NR];
 };
+using Delta = DeltaT<NMAX>;
 
 #define RTLA_NSRV(L) (NS ? NS : (L).N)
 
@@ -376,16 +391,16 @@ RTLA_HD void set_at(T* a, int j, T v) {
     if (k == j) a[k] = v;
 }
 
-template <class P>
-RTLA_HD uint64_t bag_get(const Layout& L, P row, const Delta& d, int slot) {
+template <class P, int NR>
+RTLA_HD uint64_t bag_get(const Layout& L, P row, const DeltaT<NR>& d, int slot) {
   uint64_t v = bag_slot(L, row, slot);
 #pragma unroll
   for (int q = 0; q < 3; q++)
     if (q < d.nops && d.op_slot[q] == slot) v = d.op_new[q];
   return v;
 }
-template <class P>
-RTLA_HD void bag_set(const Layout& L, P row, Delta& d, int slot, uint64_t v) {
+template <class P, int NR>
+RTLA_HD void bag_set(const Layout& L, P row, DeltaT<NR>& d, int slot, uint64_t v) {
   bool done = false;
 #pragma unroll
   for (int q = 0; q < 3; q++)
@@ -398,16 +413,16 @@ RTLA_HD void bag_set(const Layout& L, P row, Delta& d, int slot, uint64_t v) {
     if (q == d.nops) { d.op_slot[q] = slot; d.op_old[q] = old; d.op_new[q] = v; }
   d.nops++;
 }
-template <class P>
-RTLA_HD int bag_find(const Layout& L, P row, const Delta& d, uint64_t key) {
+template <class P, int NR>
+RTLA_HD int bag_find(const Layout& L, P row, const DeltaT<NR>& d, uint64_t key) {
   int hit = -1;
   for (int k = 0; k < d.nmsg; k++)
     if (hit < 0 && m_key(bag_get(L, row, d, k)) == key) hit = k;
   return hit;
 }
 // raft.tla:106-110 WithMessage
-template <class P>
-RTLA_HD void with_message(const Layout& L, P row, Delta& d, uint64_t key) {
+template <class P, int NR>
+RTLA_HD void with_message(const Layout& L, P row, DeltaT<NR>& d, uint64_t key) {
   int p = bag_find(L, row, d, key);
   if (p >= 0) {
     bag_set(L, row, d, p, bag_get(L, row, d, p) + (1ull << 60));
@@ -418,8 +433,8 @@ RTLA_HD void with_message(const Layout& L, P row, Delta& d, uint64_t key) {
   }
 }
 // raft.tla:114-119 WithoutMessage
-template <class P>
-RTLA_HD void without_message(const Layout& L, P row, Delta& d, uint64_t key) {
+template <class P, int NR>
+RTLA_HD void without_message(const Layout& L, P row, DeltaT<NR>& d, uint64_t key) {
   int p = bag_find(L, row, d, key);
   if (p < 0) return;
   uint64_t v = bag_get(L, row, d, p);
@@ -440,20 +455,22 @@ RTLA_HD void without_message(const Layout& L, P row, Delta& d, uint64_t key) {
 // matters.  Every action touches at most two distinct message keys, and the
 // two keys of Reply (raft.tla:129-130) always differ in type, so each op can
 // look its key up in the PARENT bag.
-struct DeltaFp {
+template <int NR = NMAX>
+struct DeltaFpT {
   int32_t enabled;
   int32_t in_model;
   int32_t sub;
   int32_t err;
   int32_t srv;
-  uint32_t rec[3 + NMAX];
+  uint32_t rec[3 + NR];
   int32_t nmsg;            // new number of bag slots in use
   int32_t nmsg0;           // parent's
   int32_t dcount;          // change of BagCardinality(messages)
   int32_t elec;
-  uint32_t erec[2 + NMAX];
+  uint32_t erec[2 + NR];
   FP fmsg;                 // change of the message-multiset hash
 };
+using DeltaFp = DeltaFpT<NMAX>;
 
 template <class P>
 RTLA_HD int bag_find0(const Layout& L, P row, int n, uint64_t key, uint64_t* val) {
@@ -467,15 +484,16 @@ RTLA_HD int bag_find0(const Layout& L, P row, int n, uint64_t key, uint64_t* val
   return hit;
 }
 // count c -> c + dc of message `key` (c = 0: absent), for the probe pass
-RTLA_HD void fp_bag_count(const Layout& L, DeltaFp& d, uint64_t key, uint32_t c, int dc) {
+template <int NR>
+RTLA_HD void fp_bag_count(const Layout& L, DeltaFpT<NR>& d, uint64_t key, uint32_t c, int dc) {
   const uint32_t n = (uint32_t)((int)c + dc);
   if ((int)n > L.C) d.in_model = 0;
   d.dcount += dc;
   if (c) d.fmsg = fp_sub(d.fmsg, h_msg(key | (uint64_t)c << 60));
   if (n) d.fmsg = fp_add(d.fmsg, h_msg(key | (uint64_t)n << 60));
 }
-template <class P>
-RTLA_HD void with_message(const Layout& L, P row, DeltaFp& d, uint64_t key) {  // raft.tla:106-110
+template <class P, int NR>
+RTLA_HD void with_message(const Layout& L, P row, DeltaFpT<NR>& d, uint64_t key) {  // raft.tla:106-110
   uint64_t v;
   if (bag_find0(L, row, d.nmsg0, key, &v) >= 0) {
     fp_bag_count(L, d, key, m_count(v), 1);
@@ -485,29 +503,31 @@ RTLA_HD void with_message(const Layout& L, P row, DeltaFp& d, uint64_t key) {  /
     fp_bag_count(L, d, key, 0, 1);
   }
 }
-template <class P>
-RTLA_HD void without_message(const Layout& L, P row, DeltaFp& d, uint64_t key) {  // raft.tla:114-119
+template <class P, int NR>
+RTLA_HD void without_message(const Layout& L, P row, DeltaFpT<NR>& d, uint64_t key) {  // raft.tla:114-119
   uint64_t v;
   if (bag_find0(L, row, d.nmsg0, key, &v) < 0) return;
   if (m_count(v) <= 1) d.nmsg--;
   fp_bag_count(L, d, key, m_count(v), -1);
 }
-template <class P>
-RTLA_HD void bag_dup_slot(const Layout& L, P row, DeltaFp& d, int x) {  // DuplicateMessage :443-445
+template <class P, int NR>
+RTLA_HD void bag_dup_slot(const Layout& L, P row, DeltaFpT<NR>& d, int x) {  // DuplicateMessage :443-445
   const uint64_t v = bag_slot(L, row, x);
   fp_bag_count(L, d, m_key(v), m_count(v), 1);
 }
-template <class P>
-RTLA_HD void bag_dup_slot(const Layout& L, P row, Delta& d, int x) {
+template <class P, int NR>
+RTLA_HD void bag_dup_slot(const Layout& L, P row, DeltaT<NR>& d, int x) {
   bag_set(L, row, d, x, bag_slot(L, row, x) + (1ull << 60));
 }
-RTLA_HD void delta_reset(Delta& d) { d.nops = 0; }
-RTLA_HD void delta_reset(DeltaFp& d) {
+template <int NR>
+RTLA_HD void delta_reset(DeltaT<NR>& d) { d.nops = 0; }
+template <int NR>
+RTLA_HD void delta_reset(DeltaFpT<NR>& d) {
   d.nmsg0 = d.nmsg; d.dcount = 0; d.fmsg = FP{0, 0};
 }
 // message part of the state constraint (specs/MC.tla StateConstraint)
-template <class P>
-RTLA_HD void bag_constraint(const Layout& L, P row, Delta& d) {
+template <class P, int NR>
+RTLA_HD void bag_constraint(const Layout& L, P row, DeltaT<NR>& d) {
   if (!d.nops) return;
   int total_delta = 0;
 #pragma unroll
@@ -524,8 +544,8 @@ RTLA_HD void bag_constraint(const Layout& L, P row, Delta& d) {
     if (total + total_delta > L.M) d.in_model = 0;
   }
 }
-template <class P>
-RTLA_HD void bag_constraint(const Layout& L, P row, DeltaFp& d) {
+template <class P, int NR>
+RTLA_HD void bag_constraint(const Layout& L, P row, DeltaFpT<NR>& d) {
   if (L.M > 0 && d.dcount > 0) {
     int total = 0;
     for (int k = 0; k < d.nmsg0; k++) total += (int)m_count(bag_slot(L, row, k));
@@ -758,8 +778,8 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
 
 // Fingerprint change of the delta (allLogs change excluded: per parent).
 // `h_old_srv` (optional) = the parent's h_srv of server d.srv, precomputed.
-template <int NS, class P>
-RTLA_HD FP delta_fp(const Layout& L, P row, const Delta& d, const FP* h_old_srv = nullptr) {
+template <int NS, class P, int NR>
+RTLA_HD FP delta_fp(const Layout& L, P row, const DeltaT<NR>& d, const FP* h_old_srv = nullptr) {
   const int SW = 3 + RTLA_NSRV(L);
   FP f{0, 0};
   if (d.srv >= 0) {
@@ -780,8 +800,8 @@ RTLA_HD FP delta_fp(const Layout& L, P row, const Delta& d, const FP* h_old_srv 
   return f;
 }
 
-template <int NS, class P>
-RTLA_HD FP delta_fp(const Layout& L, P row, const DeltaFp& d, const FP* h_old_srv = nullptr) {
+template <int NS, class P, int NR>
+RTLA_HD FP delta_fp(const Layout& L, P row, const DeltaFpT<NR>& d, const FP* h_old_srv = nullptr) {
   const int SW = 3 + RTLA_NSRV(L);
   FP f = d.fmsg;
   if (d.srv >= 0) {
@@ -817,33 +837,46 @@ RTLA_HD FP alllogs_delta(const Layout& L, P row, Q all_out) {
   return f;
 }
 
-// Materialise the successor row: child = parent + delta, with new allLogs
-// words and fingerprint.  `child` may alias nothing in `row`.
-template <int NS, class P, class Q, class R>
-RTLA_HD void materialize(const Layout& L, P row, const Delta& d, R all_new, FP fp, Q child) {
+// The words in which the successor row (parent + delta, with the new allLogs
+// words and fingerprint) differs from its parent row, as put(word, value)
+// calls; every other word of the child equals the parent's.  At most
+// 4 + 1 + SW + all_words + EW + 6 words.
+template <int NS, class P, class R, class F, int NR>
+RTLA_HD void child_patches(const Layout& L, P row, const DeltaT<NR>& d, R all_new, FP fp, F put) {
   const int SW = 3 + RTLA_NSRV(L), EW = 2 + RTLA_NSRV(L);
-  for (int w = 0; w < L.W; w++) child[w] = row[w];
-  row_set_fp(child, fp);
+  put(0, (uint32_t)fp.a);
+  put(1, (uint32_t)(fp.a >> 32));
+  put(2, (uint32_t)fp.b);
+  put(3, (uint32_t)(fp.b >> 32));
   const int ne = row_nelec(L, row) + (d.elec ? 1 : 0);
-  child[L.off_hdr] = (uint32_t)d.nmsg | (uint32_t)ne << 8;
+  put(L.off_hdr, (uint32_t)d.nmsg | (uint32_t)ne << 8);
   if (d.srv >= 0) {
 #pragma unroll
     for (int w = 0; w < 3 + (NS ? NS : NMAX); w++)
-      if (w < SW) child[L.off_srv + d.srv * SW + w] = d.rec[w];
+      if (w < SW) put(L.off_srv + d.srv * SW + w, d.rec[w]);
   }
-  for (int w = 0; w < L.all_words; w++) child[L.off_all + w] = all_new[w];
+  for (int w = 0; w < L.all_words; w++) put(L.off_all + w, all_new[w]);
   if (d.elec) {
 #pragma unroll
     for (int w = 0; w < 2 + (NS ? NS : NMAX); w++)
-      if (w < EW) child[L.off_elec + (ne - 1) * EW + w] = d.erec[w];
+      if (w < EW) put(L.off_elec + (ne - 1) * EW + w, d.erec[w]);
   }
 #pragma unroll
   for (int q = 0; q < 3; q++) {
     if (q < d.nops) {
-      child[L.off_bag + 2 * d.op_slot[q]] = (uint32_t)d.op_new[q];
-      child[L.off_bag + 2 * d.op_slot[q] + 1] = (uint32_t)(d.op_new[q] >> 32);
+      put(L.off_bag + 2 * d.op_slot[q], (uint32_t)d.op_new[q]);
+      put(L.off_bag + 2 * d.op_slot[q] + 1, (uint32_t)(d.op_new[q] >> 32));
     }
   }
+}
+
+// Materialise the successor row: child = parent + child_patches.
+// `child` may alias `row` (in place) but nothing else of it.
+template <int NS, class P, class Q, class R, int NR>
+RTLA_HD void materialize(const Layout& L, P row, const DeltaT<NR>& d, R all_new, FP fp, Q child) {
+  for (int w = 0; w < L.W; w++) child[w] = row[w];
+  // (child_patches reads the parent's nelec from the copy before it rewrites the header)
+  child_patches<NS>(L, child, d, all_new, fp, [&](int w, uint32_t v) { child[w] = v; });
 }
 
 // ------------------------------------------------------------ symmetry ----
@@ -982,8 +1015,8 @@ RTLA_HD FP perm_row_fp(const Layout& L, P row, const int* pi, const int* inv) {
 
 // fp(pi(row + d)) - fp(pi(row)): only the components the delta changes
 // (one server record, <= 3 bag slots, one appended election record).
-template <int NS, class P>
-RTLA_HD FP perm_delta_fp(const Layout& L, P row, const Delta& d, const int* pi, const int* inv) {
+template <int NS, class P, int NR>
+RTLA_HD FP perm_delta_fp(const Layout& L, P row, const DeltaT<NR>& d, const int* pi, const int* inv) {
   constexpr int SW = 3 + NS, EW = 2 + NS;
   FP f{0, 0};
   if (d.srv >= 0) {
@@ -1107,8 +1140,8 @@ RTLA_HD int check_invariants_v(const Layout& L, P row, int dsrv, uint32_t drec0,
   return bad;
 }
 
-template <int NS, class P>
-RTLA_HD int check_invariants(const Layout& L, P row, const Delta* d) {
+template <int NS, class P, int NR = NMAX>
+RTLA_HD int check_invariants(const Layout& L, P row, const DeltaT<NR>* d) {
   if (!d) return check_invariants_v<NS>(L, row, -1, 0u, 0u, 0, 0u);
   return check_invariants_v<NS>(L, row, d->srv, d->rec[0], d->rec[1], d->elec, d->erec[0]);
 }

@@ -5,7 +5,7 @@ name=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 D=$ROOT/exp/$name; mkdir -p $D
 H=/opt/rocm/bin/hipcc
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
+F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
 S=$ROOT/raft-tla_amd/csrc
 $H $F -c -o $D/k.o $S/rtla_kernels.hip &
 $H $F -c -o $D/h.o $S/rtla_host.cpp &
