@@ -243,8 +243,10 @@ class Run:
         return ck.levels
 
 
-def timed(run, steps, warmup, world, barrier):
-    if run.capped:
+def timed(run, steps, warmup, world, barrier, cap_levels=0):
+    if run.capped and cap_levels:
+        run.levels_cap, run.exhausted, run.stop = cap_levels, False, "--cap-levels %d" % cap_levels
+    elif run.capped:
         run.size()
     for _ in range(warmup):
         run.one()
@@ -259,24 +261,21 @@ def timed(run, steps, warmup, world, barrier):
 
 
 def roofline(levels, world, workload):
-    """Roofline of the dominant kernel, the probe kernel k_expand_compact,
-    from the last run's HIP-event times (expand_ms: the probe kernel alone;
-    the rest of kernel_ms is k_materialize building the new rows).
-    Algorithmic bytes of one launch over E frontier states: E*S (rows read)
-    + P*64 (one 64-B HBM transaction per fingerprint-set probe, P in-model
-    successors that differ from their parent) + D*8 (parent records)."""
+    """Roofline of the dominant kernel -- k_expand_compact, the whole BFS
+    level (expand, fingerprint, probe, insert, build the new rows) -- from
+    the last run's HIP-event times around it (expand_ms).  Algorithmic bytes
+    of one launch over E frontier states: E*S (rows read) + P*64 (one 64-B HBM
+    transaction per fingerprint-set probe, P = in-model successors that differ
+    from their parent) + D*(S+8) (new rows and their parent records written)."""
     S = levels[0].row_bytes
     lv1 = levels[1:]
     launches = len(lv1)
     ems = sum(lv.expand_ms for lv in lv1)
-    kms = sum(lv.kernel_ms for lv in lv1)
     E = sum(lv.frontier for lv in lv1)
     D = sum(lv.new for lv in lv1)
     P = sum(lv.probes for lv in lv1)
-    probe_kernel_bytes = E * S + P * 64 + D * 8
-    achieved = probe_kernel_bytes / world / (ems / 1e3) / 1e9   # per GPU
-    mat_ms = kms - ems
-    mat_bytes = D * (2 * S + 8)  # parent row read + record read + row written
+    kernel_bytes = E * S + P * 64 + D * (S + 8)
+    achieved = kernel_bytes / world / (ems / 1e3) / 1e9   # per GPU
     traffic = load_traffic(workload) if world == 1 else None
     ra_ceiling = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
     return {
@@ -286,22 +285,20 @@ def roofline(levels, world, workload):
         "traffic_source": traffic["source"] if traffic else None,
         "kernel": "k_expand_compact", "launches": launches, "kernel_ms_total": ems,
         "kernel_ms_avg": ems / max(1, launches),
-        "bytes_per_launch": probe_kernel_bytes / max(1, launches),
-        "bytes_per_frontier_state": probe_kernel_bytes / max(1, E),
-        "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + 8 B per new parent record",
+        "bytes_per_launch": kernel_bytes / max(1, launches),
+        "bytes_per_frontier_state": kernel_bytes / max(1, E),
+        "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + D*(S+8) new rows and parent records",
         "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
                           "frac": P / world / (ems / 1e3) / ra_ceiling,
                           "model": "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S)",
                           "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)"},
-        "k_materialize": {"ms_total": mat_ms, "bytes": mat_bytes,
-                          "GB_per_s": mat_bytes / world / (mat_ms / 1e3) / 1e9 if mat_ms > 0 else None},
     }
 
 
 def print_levels(name, levels):
     for lv in levels:
-        print("%s level %3d frontier %12d new %12d generated %13d kernel %9.3f ms (probe %9.3f ms)" %
-              (name, lv.level, lv.frontier, lv.new, lv.generated, lv.kernel_ms, lv.expand_ms), file=sys.stderr)
+        print("%s level %3d frontier %12d new %12d generated %13d kernel %9.3f ms" %
+              (name, lv.level, lv.frontier, lv.new, lv.generated, lv.expand_ms), file=sys.stderr)
 
 
 def main():
@@ -320,6 +317,9 @@ def main():
                     help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the workload")
     ap.add_argument("--frontier-cap", type=int, default=0, help="rows of the frontier arena per rank (0 = auto)")
     ap.add_argument("--levels", action="store_true", help="print the per-level tables to stderr")
+    ap.add_argument("--cap-levels", type=int, default=0,
+                    help="capped workloads: run exactly this many complete levels and skip the sizing run "
+                         "(profiling; a level that does not fit is still an error)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous check only: every rank joins the process group, receives rank 0's "
                          "RCCL-id payload, prints one line and exits (no GPU work; used by the CPU tests)")
@@ -361,7 +361,7 @@ def main():
 
     run = Run(rtla, args.workload, rank, world, comm_id, args, args.frontier_cap)
     info = json.loads(run.ck.device_info())
-    per_step, levels = timed(run, args.steps, args.warmup, world, barrier)
+    per_step, levels = timed(run, args.steps, args.warmup, world, barrier, args.cap_levels)
     distinct = sum(lv.new for lv in levels)
     generated = sum(lv.generated for lv in levels)
     depth = sum(1 for lv in levels if lv.new > 0)

@@ -969,6 +969,16 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
       s.viol_parent = hc[k].viol_parent; s.viol_child = hc[k].viol_child;
     }
   }
+  if (getenv("RTLA_STAMPS_PRINT")) {  // RTLA_STAMPS builds: where the level kernel's wave-cycles went
+    static const char* ph[8] = {"group", "ring", "compute", "resolve", "issue", "rows", "drain", "end"};
+    unsigned long long tot = 0;
+    for (int k = 0; k < 8; k++) tot += hc[0].stamp[k];
+    if (tot) {
+      fprintf(stderr, "stamps level %d:", x->level + 1);
+      for (int k = 0; k < 8; k++) fprintf(stderr, " %s %.3f", ph[k], (double)hc[0].stamp[k] / tot);
+      fprintf(stderr, " (%.3g wave-cycles)\n", (double)tot);
+    }
+  }
   int rc = allreduce2_u64(x, sums, 4, maxs, 4);
   if (rc) return rc;
   x->max_front = maxs[3];
