@@ -52,18 +52,26 @@ WORKLOADS = {
     "raft3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, ("NoTwoLeaders",)),
     "raft3_v1_t2_l1_m1": (3, 1, 2, 1, 1, 1, ("NoTwoLeaders",)),
 }
-BASELINE_INDEX = {"cfg1": 0, "cfg2": 1}
+# BASELINE.json configs[4]: random valid packed states in the cfg-3 layout
+# (SURVEY.md section 8(d)): 3 servers, 2 values, term <= 4, log <= 3, 2 copies
+WORKLOADS["synthetic"] = (3, 2, 4, 3, 2, 0, ES_LM)
+BASELINE_INDEX = {"cfg1": 0, "cfg2": 1, "synthetic": 4}
 CAPPED = {"cfg1", "cfg2"}          # not exhaustible on one GPU: run until HBM is full
 DEFAULT = "cfg2"
 SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run reports it too)
 # Fingerprint-set size (log2 slots) per workload: ~25-30 % load at the size reached.
 FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30,
-              "cfg2": 31, "cfg1": 31}
+              "cfg2": 31, "cfg1": 31, "synthetic": 33}
 # Bag slots per row for the unbounded-bag configs.  A state d BFS levels below
 # Init holds at most d - 1 distinct messages (every action adds at most one),
 # so this bounds the depth at which the row format -- not memory -- stops the
 # search; a successor that needs more raises RTLA_CAP_ROW, never truncates.
-BAG_CAP = {"cfg2": 18, "cfg1": 24}
+BAG_CAP = {"cfg2": 18, "cfg1": 24, "synthetic": 12}
+# Synthetic microbench: input states per GPU (1e9 over 8 GPUs), the pool half
+# of them are redrawn from (so dedup has hits), states per device batch.
+SYNTH_STATES = 125_000_000
+SYNTH_POOL_FRAC = 10
+SYNTH_BATCH = 1 << 24
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Random 8-byte fingerprint-set accesses into a 32 GiB table (far beyond the
 # 256 MiB Infinity Cache), all CUs, measured on MI355X by tools/probe_calib.py
@@ -209,6 +217,7 @@ class Run:
         self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
         self.levels_cap = None   # complete levels a capped search reaches
         self.stop = None         # what stopped the sizing run
+        self.exhausted = False
 
     def size(self):
         """Capped workloads: BFS until the next level does not fit; the timed
@@ -295,6 +304,39 @@ def roofline(levels, world, workload):
     }
 
 
+def synthetic(run, args, rank, world, barrier):
+    """BASELINE configs[4]: a step = every input state of this rank (batches of
+    SYNTH_BATCH generated on the device) through Next + fingerprint + dedup
+    into the rank's fingerprint set, cleared first.  Each rank takes its own
+    range of the input numbering; with several ranks each deduplicates what
+    it generates (independent replicas: no exchange)."""
+    n = args.synth_states
+    pool = n // SYNTH_POOL_FRAC
+    first0 = rank * n
+
+    def one():
+        run.ck.reset()
+        tot = {"generated": 0, "probes": 0, "new": 0, "kernel_ms": 0.0, "batches": 0}
+        for b in range(0, n, SYNTH_BATCH):
+            lv = run.ck.synthetic_step(first0 + b, min(SYNTH_BATCH, n - b), pool)
+            tot["generated"] += lv.generated
+            tot["probes"] += lv.probes
+            tot["new"] += lv.new
+            tot["kernel_ms"] += lv.kernel_ms
+            tot["batches"] += 1
+        return tot
+
+    for _ in range(args.warmup):
+        one()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tot = one()
+    t1 = time.perf_counter()
+    barrier()
+    return max_over_ranks(t1 - t0, world) / args.steps, tot, pool
+
+
 def print_levels(name, levels):
     for lv in levels:
         print("%s level %3d frontier %12d new %12d generated %13d kernel %9.3f ms" %
@@ -317,6 +359,8 @@ def main():
                     help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the workload")
     ap.add_argument("--frontier-cap", type=int, default=0, help="rows of the frontier arena per rank (0 = auto)")
     ap.add_argument("--levels", action="store_true", help="print the per-level tables to stderr")
+    ap.add_argument("--synth-states", type=int, default=SYNTH_STATES,
+                    help="synthetic workload: input states per GPU")
     ap.add_argument("--cap-levels", type=int, default=0,
                     help="capped workloads: run exactly this many complete levels and skip the sizing run "
                          "(profiling; a level that does not fit is still an error)")
@@ -361,6 +405,43 @@ def main():
 
     run = Run(rtla, args.workload, rank, world, comm_id, args, args.frontier_cap)
     info = json.loads(run.ck.device_info())
+    if args.workload == "synthetic":
+        per_step, tot, pool = synthetic(run, args, rank, world, barrier)
+        S = run.ck.levels[0].row_bytes if run.ck.levels else 4 * rtla.row_words(run.cfg)
+        n = args.synth_states
+        ems = tot["kernel_ms"]
+        P, D = tot["probes"], tot["new"]
+        kbytes = n * S + P * 64
+        ra = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
+        out = {
+            "metric": "random packed states/sec through Next + fingerprint + dedup (BASELINE configs[4])",
+            "value": n * world / per_step, "unit": "input states/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": per_step * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: counter-based PRNG (seed 0x5AF72025) valid random states, 1/2 redrawn from a pool",
+            "config": {"workload": "synthetic", "baseline_config": 4, "layout": "cfg-3: N3 V2 T4 L3 C2, bag_cap 12",
+                       "input_states_per_gpu": n, "pool": pool, "batch": SYNTH_BATCH, "batches": tot["batches"],
+                       "generated": tot["generated"], "probes": P, "distinct_successors": D,
+                       "successors_per_s": tot["generated"] * world / per_step, "row_bytes": S,
+                       "fpset_slots_log2": run.fpl,
+                       "parallelism": "single" if world == 1 else "replicas%d" % world},
+            "roofline": {"bound": "hbm", "achieved": kbytes / (ems / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": kbytes / (ems / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_expand_compact (XF_DEDUP_ONLY)", "launches": tot["batches"],
+                         "kernel_ms_total": ems, "kernel_ms_avg": ems / max(1, tot["batches"]),
+                         "bytes_per_launch": kbytes / max(1, tot["batches"]),
+                         "model": "per launch: E*S input rows read + 64 B per fingerprint-set probe",
+                         "random_access": {"probes_per_s": P / (ems / 1e3), "ceiling_per_s": ra,
+                                           "frac": P / (ems / 1e3) / ra}},
+            "cpu_baseline": None,
+        }
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        run.ck.close()
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     per_step, levels = timed(run, args.steps, args.warmup, world, barrier, args.cap_levels)
     distinct = sum(lv.new for lv in levels)
     generated = sum(lv.generated for lv in levels)

@@ -17,11 +17,14 @@
 // 12 = safety violation, 150/151 = spec/config errors, 255 = other errors
 // (TLC's ExitStatus values as we understand them; not verified against a
 // live TLC here).
+#include <spawn.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/wait.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <filesystem>
@@ -32,6 +35,8 @@
 #include <vector>
 
 #include "../../include/rtla.h"
+
+extern char** environ;
 
 static const char* RAFT_SHA256 = "683a120af29e3e5a805e291f756229d65914f8fb73dddd8c78bafef50a6f6b81";
 
@@ -213,6 +218,74 @@ std::string subst_names(const std::string& s, const std::vector<std::string>& se
   return o;
 }
 
+// ---- -gpus N: one process per GPU.  The launcher (this process, which never
+// touches a GPU) spawns N copies of itself with RTLA_RANK / RTLA_WORLD /
+// RTLA_RENDEZVOUS in the environment and relays rank 0's exit status.  Rank 0
+// creates the RCCL unique id and publishes it through the rendezvous file;
+// every rank opens its context with it (rtla_open, one shard per rank).
+int launch_ranks(int n, char** argv) {
+  char dir[] = "/tmp/rtla-rdv-XXXXXX";
+  if (!mkdtemp(dir)) { perror("mkdtemp"); return 255; }
+  const std::string rdv = std::string(dir) + "/comm_id";
+  std::vector<pid_t> pids;
+  for (int r = 0; r < n; r++) {
+    std::vector<std::string> env;
+    for (char** e = environ; *e; e++)
+      if (strncmp(*e, "RTLA_RANK=", 10) && strncmp(*e, "RTLA_WORLD=", 11) && strncmp(*e, "RTLA_RENDEZVOUS=", 16))
+        env.push_back(*e);
+    env.push_back("RTLA_RANK=" + std::to_string(r));
+    env.push_back("RTLA_WORLD=" + std::to_string(n));
+    env.push_back("RTLA_RENDEZVOUS=" + rdv);
+    std::vector<char*> envp;
+    for (auto& e : env) envp.push_back((char*)e.c_str());
+    envp.push_back(nullptr);
+    pid_t pid = 0;
+    if (posix_spawn(&pid, "/proc/self/exe", nullptr, nullptr, argv, envp.data()) != 0) {
+      perror("posix_spawn");
+      return 255;
+    }
+    pids.push_back(pid);
+  }
+  int code0 = 0, worst = 0;
+  for (int r = 0; r < n; r++) {
+    int st = 0;
+    waitpid(pids[r], &st, 0);
+    const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 255;
+    if (r == 0) code0 = code;
+    else if (code && !worst) worst = code;
+  }
+  (void)remove(rdv.c_str());
+  (void)rmdir(dir);
+  return code0 ? code0 : worst;
+}
+
+// This rank's RCCL id: rank 0 makes it (dry run: a fixed pattern, no GPU) and
+// publishes it atomically (write + rename); the others wait for the file.
+bool rendezvous(int rank, const char* path, bool dry, unsigned char id[128]) {
+  if (rank == 0) {
+    if (dry) {
+      for (int k = 0; k < 128; k++) id[k] = (unsigned char)k;
+    } else if (rtla_comm_id(id) != RTLA_OK) {
+      return false;
+    }
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f || fwrite(id, 1, 128, f) != 128) return false;
+    if (fclose(f) != 0 || rename(tmp.c_str(), path) != 0) return false;
+    return true;
+  }
+  for (int t = 0; t < 1200; t++) {  // up to 120 s
+    FILE* f = fopen(path, "rb");
+    if (f) {
+      const bool ok = fread(id, 1, 128, f) == 128;
+      fclose(f);
+      if (ok) return true;
+    }
+    usleep(100000);
+  }
+  return false;
+}
+
 const char* COVER[] = {"Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
                        "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage", "DropMessage",
                        "UpdateTerm", "HandleRequestVoteRequest", "HandleRequestVoteResponse",
@@ -251,6 +324,24 @@ int main(int argc, char** argv) {
     else spec = a;
   }
   (void)workers;
+  if (gpus < 1) { usage(); return 255; }
+  if (gpus > 1 && !getenv("RTLA_RANK")) return launch_ranks(gpus, argv);
+  const int rank = getenv("RTLA_RANK") ? atoi(getenv("RTLA_RANK")) : 0;
+  const int world = getenv("RTLA_WORLD") ? atoi(getenv("RTLA_WORLD")) : 1;
+  if (world != gpus || rank < 0 || rank >= world) {
+    fprintf(stderr, "Error: rank %d of %d does not match -gpus %d\n", rank, world, gpus);
+    return 255;
+  }
+  if (rank > 0 && !freopen("/dev/null", "w", stdout)) return 255;  // rank 0 prints TLC's output
+  const bool dry = getenv("RTLA_CLI_DRYRUN") != nullptr;
+  if (dry) {  // launch / rendezvous check only (CPU tests)
+    unsigned char id[128];
+    const char* rdv = getenv("RTLA_RENDEZVOUS");
+    const bool ok = world == 1 || (rdv && rendezvous(rank, rdv, true, id));
+    fprintf(stderr, "rtla rank %d of %d ready (id %02x%02x%02x%02x)\n", rank, world, ok ? id[0] : 255, ok ? id[1] : 255,
+            ok ? id[2] : 255, ok ? id[3] : 255);
+    return ok ? 0 : 255;
+  }
   if (spec.empty()) { usage(); return 255; }
   if (cfgpath.empty()) {
     cfgpath = spec.substr(0, spec.size() > 4 && spec.compare(spec.size() - 4, 4, ".tla") == 0 ? spec.size() - 4 : spec.size()) + ".cfg";
@@ -359,16 +450,18 @@ int main(int argc, char** argv) {
       return 151;
     }
   }
-  if (gpus != 1) {
-    printf("Error: -gpus %d: multi-GPU runs use one process per GPU (see INTEGRATION.md)\n", gpus);
+  unsigned char comm_id[128];
+  if (world > 1 && !rendezvous(rank, getenv("RTLA_RENDEZVOUS"), false, comm_id)) {
+    fprintf(stderr, "Error: rank %d: RCCL rendezvous failed\n", rank);
     return 255;
   }
   rtla_ctx* ctx = nullptr;
-  int st = rtla_open(&c, 0, 1, nullptr, &ctx);
+  int st = rtla_open(&c, rank, world, world > 1 ? comm_id : nullptr, &ctx);
   if (st < 0) { printf("Error: %s\n", rtla_strerror(st)); return 255; }
   char info[1024];
   rtla_device_info(ctx, info, sizeof info);
-  printf("Running breadth-first search Model-Checking with 128-bit fingerprints on 1 GPU: %s\n", info);
+  printf("Running breadth-first search Model-Checking with 128-bit fingerprints on %d GPU%s: %s\n", world,
+         world > 1 ? "s (fingerprint-sharded, RCCL)" : "", info);
   printf("Starting... (%s)\n", now_str().c_str());
   printf("Computing initial states...\n");
   auto t0 = std::chrono::steady_clock::now();
@@ -383,11 +476,18 @@ int main(int argc, char** argv) {
     printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
   }
   auto last_progress = t0, last_ckpt = t0;
+  // With several ranks the checkpoint (a collective) must be decided alike
+  // everywhere: the clock is then the job's device time (the per-level
+  // maximum over ranks, identical on every rank), not this rank's wall clock.
+  double dev_s = 0, dev_ckpt = 0;
   while (st == RTLA_OK) {
     st = rtla_step(ctx, &ls);
     if (st < 0) break;
-    if (ckpt_minutes > 0 && st == RTLA_OK &&
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count() >= ckpt_minutes * 60) {
+    dev_s += ls.kernel_ms / 1e3;
+    const double since = world > 1 ? dev_s - dev_ckpt
+                                   : std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count();
+    if (ckpt_minutes > 0 && st == RTLA_OK && since >= ckpt_minutes * 60) {
+      dev_ckpt = dev_s;
       // in-process (no shell from a GPU-initialised process)
       std::error_code ec;
       if (ckpt_prefix.find('/') != std::string::npos)

@@ -76,6 +76,7 @@ enum {
   XF_CAS_ONLY = 1024,     // compact kernel: probe with CAS only (no load-first)
   XF_WAVE_KERNEL = 2048,  // use the wave-per-state k_expand (the SYMMETRY path) without symmetry
   XF_NO_SPECIAL = 4096,   // compact kernel: run-time layout even for a compiled-in configuration
+  XF_DEDUP_ONLY = 8192,   // compact kernel: count new fingerprints, build no rows (synthetic microbench)
 };
 
 // Per-level device counters (zeroed before each level except `cover`).

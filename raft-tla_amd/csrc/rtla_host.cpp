@@ -50,6 +50,7 @@
 #include "rtla_device.h"
 #include "rtla_launch.h"
 #include "rtla_model.h"
+#include "rtla_synth.h"
 #include "rtla_text.h"
 
 using namespace rtla;
@@ -315,6 +316,16 @@ extern "C" int rtla_expand_batch(const rtla_cfg* c, const uint32_t* rows, size_t
   if (inf.size() > cap) return RTLA_E_ARG;
   if (succ) memcpy(succ, out.data(), out.size() * 4);
   if (info) memcpy(info, inf.data(), inf.size() * 8);
+  return RTLA_OK;
+}
+
+extern "C" int rtla_random_rows(const rtla_cfg* c, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
+                                uint32_t* rows) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  if (!rows && n) return RTLA_E_ARG;
+  for (uint64_t k = 0; k < n; k++) random_state(L, seed, synth_state_id(seed, first + k, pool), rows + k * L.W);
   return RTLA_OK;
 }
 
@@ -1154,6 +1165,45 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
   }
   (void)hipFree(d_row);
   return rc;
+}
+
+// Synthetic microbench step (BASELINE configs[4]): generate input states
+// [first, first + n) into the row arena on the device (k_random_rows), then
+// one launch of the level kernel over them in dedup-only mode: Next,
+// fingerprint, probe/insert into this context's fingerprint set, no rows kept.
+// The set accumulates across calls (rtla_reset clears it).
+extern "C" int rtla_synthetic_step(rtla_ctx* x, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
+                                   rtla_level_stats* st) {
+  if (!x || !st) return RTLA_E_ARG;
+  if (x->sh.size() != 1 || x->nshard != 1 || x->inited) return RTLA_E_STATE;
+  if (n > x->front_cap) return RTLA_E_OVERFLOW;
+  const double t0 = now_s();
+  HIPCHK(hipSetDevice(x->device));
+  Shard& s = x->sh[0];
+  HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
+  s.h_caps[0] = n; s.h_caps[1] = 0; s.h_caps[2] = s.parents_cap;
+  HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(launch_random_rows(x->L, seed, first, n, pool, s.arena, x->stream));
+  const Ring ring{s.arena, 0, x->front_cap};
+  ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+  HIPCHK(hipEventRecord(s.ev0, x->stream));
+  HIPCHK(launch_expand(x->L, ring, 0, n, 0, ring, s.parents, 0, 0, s.table, x->tlog2, s.ctr, box, x->grid,
+                       x->stream, env_xflags() | XF_DEDUP_ONLY));
+  HIPCHK(hipEventRecord(s.ev1, x->stream));
+  DevCounters h;
+  HIPCHK(hipMemcpyAsync(&h, s.ctr, sizeof h, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, s.ev0, s.ev1));
+  memset(st, 0, sizeof *st);
+  st->frontier = n; st->new_states = h.next_count; st->generated = h.generated; st->probes = h.probes;
+  st->kernel_ms = ms; st->expand_ms = ms; st->row_bytes = (uint64_t)x->L.W * 4; st->flags = h.flags;
+  st->seconds = now_s() - t0;
+  if (h.flags) {
+    report_flags(h.flags);
+    return flags_to_status(h.flags);
+  }
+  return RTLA_OK;
 }
 
 // Diagnostic: re-expand the current frontier `reps` times with the given

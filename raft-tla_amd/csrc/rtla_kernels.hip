@@ -23,6 +23,7 @@
 
 #include "rtla_device.h"
 #include "rtla_model.h"
+#include "rtla_synth.h"
 
 using namespace rtla;
 
@@ -520,16 +521,17 @@ __device__ __forceinline__ const Layout& pick_layout(const Layout& rt) {
 }
 
 // RTLA_STAMPS (diagnostic builds only): per-wave cycle counts of the level
-// kernel's phases, read from the 20-bit SHADER_CYCLES register (no memory
-// wait, unlike s_memtime) and summed into DevCounters::stamp.
+// kernel's phases from s_memtime (each stamp waits for the wave's LDS
+// operations in flight: a perturbation, fine for shares) summed into
+// DevCounters::stamp.
 #ifdef RTLA_STAMPS
 #define RTLA_STAMP_DECL                                                   \
-  uint32_t st_prev_ = __builtin_amdgcn_s_getreg(29 | (19 << 11));          \
+  unsigned long long st_prev_ = __builtin_amdgcn_s_memtime();              \
   unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define STAMP(k)                                                             \
   do {                                                                       \
-    const uint32_t t_ = __builtin_amdgcn_s_getreg(29 | (19 << 11));          \
-    st_acc_[k] += (t_ - st_prev_) & 0xfffffu;                                \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+    st_acc_[k] += t_ - st_prev_;                                             \
     st_prev_ = t_;                                                           \
   } while (0)
 #define RTLA_STAMP_FLUSH(ctr, lane)                                          \
@@ -590,6 +592,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // (mod NEWCAP) holds their parent records; their parents are rows of the
   // current group (uniform counters).
   int head = 0, tail = 0;
+  unsigned long long dedup_new = 0;  // XF_DEDUP_ONLY: new fingerprints (uniform)
   unsigned long long s0 = 0;  // first state of the current group
 #ifdef RTLA_PFP_SHFL
   FP pfp0{0, 0}, pfp{0, 0};
@@ -738,7 +741,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       }
     }
     const unsigned long long m = __ballot(isnew);
-    if (m) {
+    if (m && (xflags & XF_DEDUP_ONLY)) {  // synthetic microbench: count, keep no row
+      dedup_new += __popcll(m);
+    } else if (m) {
       if (isnew) newl[(tail + __popcll(m & lanes_below)) & (NEWCAP - 1)] = prec;
       tail += __popcll(m);
       wave_sync();
@@ -940,6 +945,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   }
   if (lane == 0 && my_gen) atomicAdd(&ctr->generated, (unsigned long long)my_gen);
   if (lane == 0 && my_probe) atomicAdd(&ctr->probes, (unsigned long long)my_probe);
+  if (lane == 0 && dedup_new) atomicAdd(&ctr->next_count, dedup_new);
   STAMP(7);
   RTLA_STAMP_FLUSH(ctr, lane)
   __syncthreads();
@@ -1195,6 +1201,25 @@ k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n
   }
 }
 
+// Synthetic microbench input (BASELINE configs[4], rtla_synth.h): input states
+// first .. first + n - 1 as rows 0 .. n - 1 of `out`.  One lane builds one
+// row in LDS; the wave stores its 64 rows with coalesced stores.
+__global__ void __launch_bounds__(64)
+k_random_rows(Layout L, unsigned long long seed, unsigned long long first, unsigned long long n,
+              unsigned long long pool, uint32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int W = L.W;
+  for (unsigned long long g = (unsigned long long)blockIdx.x * 64; g < n; g += (unsigned long long)gridDim.x * 64) {
+    const int nv = (int)min<unsigned long long>(64ull, n - g);
+    if (lane < nv) random_state(L, seed, synth_state_id(seed, first + g + lane, pool), lds + lane * W);
+    wave_sync();
+    uint32_t* dst = out + g * (unsigned long long)W;
+    for (int w = lane; w < nv * W; w += 64) dst[w] = lds[w];
+    wave_sync();
+  }
+}
+
 // Microbenchmark kernel: random 8-B CAS inserts into a table (calibrates the
 // random-access roofline of the fingerprint set).
 __global__ void k_probe_bench(unsigned long long* table, int tlog2, unsigned long long n, unsigned long long seed,
@@ -1428,6 +1453,16 @@ hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n
   int grid = (int)(blocks < 4096 ? blocks : 4096);
   RTLA_DISPATCH_N(L, k_expand_batch, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, rows,
                   (unsigned long long)n, out, (unsigned long long*)info, (unsigned long long)cap, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_random_rows(const Layout& L, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, uint32_t* out,
+                              hipStream_t st) {
+  if (!n) return hipSuccess;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + 63) / 64, 256 * 32);
+  hipLaunchKernelGGL(k_random_rows, dim3(blocks), dim3(64), (size_t)64 * L.W * sizeof(uint32_t), st, L,
+                     (unsigned long long)seed, (unsigned long long)first, (unsigned long long)n,
+                     (unsigned long long)pool, out);
   return hipGetLastError();
 }
 

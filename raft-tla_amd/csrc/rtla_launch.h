@@ -37,6 +37,8 @@ hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n,
                               int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st);
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,
                                uint64_t* info, uint64_t cap, DevCounters* ctr, hipStream_t st);
+hipError_t launch_random_rows(const Layout& L, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, uint32_t* out,
+                              hipStream_t st);
 hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed,
                               DevCounters* ctr, hipStream_t st, int load_first = 0);
 

@@ -95,6 +95,8 @@ def _load():
         "rtla_abi_version": (C.c_int, []),
         "rtla_comm_id": (C.c_int, [C.c_void_p]),
         "rtla_probe_bench": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_uint64)]),
+        "rtla_random_rows": (C.c_int, [P(_Cfg), C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, P(C.c_uint32)]),
+        "rtla_synthetic_step": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, P(_Stats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -109,7 +111,9 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
-            "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover"]
+            "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step"]
+
+SYNTH_SEED = 0x5AF72025  # the synthetic microbench's PRNG seed
 
 
 @dataclass(frozen=True)
@@ -227,6 +231,16 @@ def row_fingerprint(cfg: Config, row: Sequence[int]):
 
 def stored_fingerprint(row: Sequence[int]):
     return row[0] | row[1] << 32, row[2] | row[3] << 32
+
+
+def random_rows(cfg: Config, first: int, n: int, pool: int = 0, seed: int = SYNTH_SEED):
+    """Rows of the synthetic microbench's input states first .. first + n - 1
+    (rtla_synth.h; computed on the host)."""
+    w = row_words(cfg)
+    cc = cfg.c()
+    buf = (C.c_uint32 * max(1, n * w))()
+    _check(_lib.rtla_random_rows(C.byref(cc), seed, first, n, pool, buf), "rtla_random_rows")
+    return [list(buf[k * w:(k + 1) * w]) for k in range(n)]
 
 
 def expand_batch(cfg: Config, rows: Sequence[Sequence[int]]):
@@ -372,6 +386,16 @@ class Checker:
         ms = C.c_double()
         _check(_lib.rtla_time_expand(self._h, xflags, reps, C.byref(ms)), "rtla_time_expand")
         return ms.value
+
+    def synthetic_step(self, first: int, n: int, pool: int = 0, seed: int = SYNTH_SEED) -> Level:
+        """BASELINE configs[4]: n random states through Next + fingerprint +
+        dedup (one level-kernel launch; the set accumulates across calls)."""
+        st = _Stats()
+        rc = _lib.rtla_synthetic_step(self._h, seed, first, n, pool, C.byref(st))
+        if rc < 0:
+            raise RtlaError(rc, "rtla_synthetic_step", st.flags)
+        return Level(0, st.frontier, st.new_states, st.generated, st.seconds, st.kernel_ms, st.probes, st.row_bytes,
+                     st.expand_ms)
 
     def coverage(self) -> dict:
         n = len(COVER_NAMES)

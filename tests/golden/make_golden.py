@@ -44,29 +44,35 @@ SYM_CASES = {
 }
 # Models too large for the CPU oracle to exhaust here: a bounded prefix of
 # complete BFS levels (the oracle stops after the first level that passes
-# max_distinct).  name: (N, V, T, L, C, M, invariants, max_distinct)
+# max_distinct), with each level's state-text hash.
+# name: (N, V, T, L, C, M, invariants, max_distinct)
 PREFIXES = {
-    "n3_v2_t2_l2_m2_prefix": (3, 2, 2, 2, 1, 2, (ES, LM), 60_000_000),
+    # bench.py's exhaust model (wall time to exhaust)
+    "n3_v2_t2_l2_m2_prefix": (3, 2, 2, 2, 1, 2, (ES, LM), 200_000_000),
+    # BASELINE.json configs[1] and configs[0] exactly as stated (no in-flight bound)
+    "n3_v2_t3_l2_c1_prefix": (3, 2, 3, 2, 1, 0, (ES, LM), 25_000_000),
+    "n3_v1_t2_l1_c1_prefix": (3, 1, 2, 1, 1, 0, (NTL,), 30_000_000),
 }
 
 
 def main():
     big = "--big" in sys.argv
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
+    only = set(only[0].split(",")) if only else None
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bfs_counts.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
     raft_cpu.build()
     for name, (n, v, t, l, c, m, inv, py, is_big) in CASES.items():
-        if is_big and not big:
+        if (is_big and not big) or (only and name not in only):
             continue
         cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv)
-        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big, text_hash=not is_big)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big, text_hash=True)
         assert r["rc"] >= 0, (name, r["rc"])
         case = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c,
                 "max_msgs": m, "invariants": list(inv), "distinct": r["distinct"],
                 "generated": r["generated"], "depth": r["depth"], "levels": r["levels"],
-                "violated": r["violated"], "trace_len": r["trace_len"], "source": "oracle/raft_cpu.c"}
-        if not is_big:
-            case["level_text_hash"] = ["%016x" % h for h in r["level_text_hash"]]
+                "violated": r["violated"], "trace_len": r["trace_len"], "source": "oracle/raft_cpu.c",
+                "level_text_hash": ["%016x" % h for h in r["level_text_hash"]]}
         if py:
             pc = rv.Cfg(n, v, t, l, c, inv, m)
             pr = rv.bfs(pc)
@@ -79,7 +85,7 @@ def main():
         out[name] = case
         print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
     for name, (n, v, t, l, c, m, inv, py, is_big) in SYM_CASES.items():
-        if is_big and not big:
+        if (is_big and not big) or (only and name not in only):
             continue
         cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, symmetry=True)
         r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big)
@@ -95,14 +101,15 @@ def main():
         out[name] = case
         print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
     for name, (n, v, t, l, c, m, inv, cap) in PREFIXES.items():
-        if not big:
+        if not big or (only and name not in only):
             continue
         cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap)
-        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, text_hash=True)
         assert r["rc"] in (0, -4), (name, r["rc"])
         out[name] = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
                      "invariants": list(inv), "prefix": True, "levels": r["levels"],
-                     "distinct": r["distinct"], "generated": r["generated"],
+                     "distinct": r["distinct"], "generated": r["generated"], "max_msgs_seen": r["max_msgs"],
+                     "level_text_hash": ["%016x" % h for h in r["level_text_hash"]],
                      "source": "oracle/raft_cpu.c, first %d complete levels" % len(r["levels"])}
         print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
     with open(path, "w") as f:
