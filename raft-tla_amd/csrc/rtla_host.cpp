@@ -877,6 +877,19 @@ static int move_rows(rtla_ctx* x, uint64_t lo) {
   return RTLA_OK;
 }
 
+// RTLA_STAMPS builds with RTLA_STAMPS_PRINT set: where the level kernel's
+// wave-cycles went (diagnostic).
+static void print_stamps(const DevCounters& c, int level) {
+  if (!getenv("RTLA_STAMPS_PRINT")) return;
+  static const char* ph[8] = {"group", "ring", "compute", "resolve", "issue", "rows", "drain", "end"};
+  unsigned long long tot = 0;
+  for (int k = 0; k < 8; k++) tot += c.stamp[k];
+  if (!tot) return;
+  fprintf(stderr, "stamps level %d:", level);
+  for (int k = 0; k < 8; k++) fprintf(stderr, " %s %.3f", ph[k], (double)c.stamp[k] / tot);
+  fprintf(stderr, " (%.3g wave-cycles)\n", (double)tot);
+}
+
 extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   if (!x) return RTLA_E_ARG;
   if (!x->inited || x->finished) return RTLA_E_STATE;
@@ -980,16 +993,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
       s.viol_parent = hc[k].viol_parent; s.viol_child = hc[k].viol_child;
     }
   }
-  if (getenv("RTLA_STAMPS_PRINT")) {  // RTLA_STAMPS builds: where the level kernel's wave-cycles went
-    static const char* ph[8] = {"group", "ring", "compute", "resolve", "issue", "rows", "drain", "end"};
-    unsigned long long tot = 0;
-    for (int k = 0; k < 8; k++) tot += hc[0].stamp[k];
-    if (tot) {
-      fprintf(stderr, "stamps level %d:", x->level + 1);
-      for (int k = 0; k < 8; k++) fprintf(stderr, " %s %.3f", ph[k], (double)hc[0].stamp[k] / tot);
-      fprintf(stderr, " (%.3g wave-cycles)\n", (double)tot);
-    }
-  }
+  print_stamps(hc[0], x->level + 1);
   int rc = allreduce2_u64(x, sums, 4, maxs, 4);
   if (rc) return rc;
   x->max_front = maxs[3];
@@ -1195,6 +1199,7 @@ extern "C" int rtla_synthetic_step(rtla_ctx* x, uint64_t seed, uint64_t first, u
   HIPCHK(hipStreamSynchronize(x->stream));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, s.ev0, s.ev1));
+  print_stamps(h, 0);
   memset(st, 0, sizeof *st);
   st->frontier = n; st->new_states = h.next_count; st->generated = h.generated; st->probes = h.probes;
   st->kernel_ms = ms; st->expand_ms = ms; st->row_bytes = (uint64_t)x->L.W * 4; st->flags = h.flags;

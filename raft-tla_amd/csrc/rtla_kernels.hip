@@ -131,6 +131,20 @@ __device__ __forceinline__ int fpset_insert(unsigned long long* table, int log2,
 
 __device__ __forceinline__ void set_flag(DevCounters* c, int f) { atomicOr(&c->flags, f); }
 
+// The first violation found wins and is never replaced.  Called by the whole
+// wave (bad = this lane's violated-invariant mask, 0 if none): one CAS per
+// wave -- its first violating lane -- and none once a violation has been
+// recorded, so successors that all violate an invariant (random states, or
+// a violation reached by many parents) do not serialise on that one word.
+// Returns true on the lane whose violation was recorded.
+__device__ __forceinline__ bool claim_violation(DevCounters* c, int bad, int lane) {
+  const unsigned long long m = __ballot(bad != 0);
+  if (!m) return false;
+  if (lane != __builtin_ctzll(m)) return false;
+  if (__hip_atomic_load(&c->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+  return atomicCAS(&c->viol_mask, 0, bad) == 0;
+}
+
 // Finish an insert whose home slot `idx` was READ (not CAS'd) as `seen`.
 // Slots only ever change 0 -> key, so a slot holding the key proves the
 // state is present, and one holding another key can be skipped for good;
@@ -369,7 +383,8 @@ k_expand(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_en
       }
       if (en && (isnew || !d.in_model)) {
         int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-        if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+        if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
           ctr->viol_parent = cur_base + s;
           ctr->viol_inst = inst;
           ctr->viol_in_model = d.in_model;
@@ -654,16 +669,17 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     const FP qfp = pfpl[sl];
 #endif
     FP cfp{0, 0};
+    int bad = 0;
     if (act) {
       const uint32_t* prow = rows + sl * W;
       cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
-      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-      if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-        ctr->viol_parent = cur_base + s0 + sl;
-        ctr->viol_inst = inst;
-        ctr->viol_in_model = 1;
-        ctr->viol_child = lane < nrows ? next_base + obase + lane : ~0ull;
-      }
+      bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+    }
+    if (claim_violation(ctr, bad, lane)) {
+      ctr->viol_parent = cur_base + s0 + sl;
+      ctr->viol_inst = inst;
+      ctr->viol_in_model = 1;
+      ctr->viol_child = lane < nrows ? next_base + obase + lane : ~0ull;
     }
     if (!(xflags & XF_NO_COVER)) {  // distinct coverage, aggregated over equal codes
       const int code = act ? cover_code(L, inst, d.sub) : -1;
@@ -886,14 +902,16 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
             if (en && !same) atomicAdd(&cov[code], 1u);
           }
         }
-        if (en && !d.in_model) {  // out-of-model successors: checked, never stored
-          const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-          if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-            ctr->viol_parent = cur_base + s0 + sl;
-            ctr->viol_inst = inst;
-            ctr->viol_in_model = 0;
-            ctr->viol_child = ~0ull;
-          }
+        // out-of-model successors: checked, never stored (not in the
+        // synthetic microbench, whose random states are no model's)
+        int bad = 0;
+        if (en && !d.in_model && !(xflags & XF_DEDUP_ONLY))
+          bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+        if (claim_violation(ctr, bad, lane)) {
+          ctr->viol_parent = cur_base + s0 + sl;
+          ctr->viol_inst = inst;
+          ctr->viol_in_model = 0;
+          ctr->viol_child = ~0ull;
         }
         STAMP(2);  // successor deltas, fingerprints, coverage, out-of-model invariants
         resolve();  // the previous chunk's probes, after this chunk's arithmetic
@@ -1057,7 +1075,8 @@ k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
       compute_delta<NS>(L, prow, inst, d);
       const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
       const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-      if (bad && atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+      if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
         ctr->viol_parent = cur_base + s;
         ctr->viol_inst = inst;
         ctr->viol_in_model = 1;
