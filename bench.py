@@ -52,21 +52,27 @@ WORKLOADS = {
     "raft3_v1_t2_l1_m2": (3, 1, 2, 1, 1, 2, ("NoTwoLeaders",)),
     "raft3_v1_t2_l1_m1": (3, 1, 2, 1, 1, 1, ("NoTwoLeaders",)),
 }
+# BASELINE.json configs[2] (dup/drop live: 2 copies per message) and configs[3]
+# (5 servers under SYMMETRY Permutations(Server)), as stated; both are capped
+# by device memory like cfg1/cfg2.  configs[3] names no invariant.
+WORKLOADS["cfg3"] = (3, 2, 4, 3, 2, 0, ())
+WORKLOADS["cfg4"] = (5, 1, 3, 2, 1, 0, ())
+SYMMETRIC = {"cfg4"}
 # BASELINE.json configs[4]: random valid packed states in the cfg-3 layout
 # (SURVEY.md section 8(d)): 3 servers, 2 values, term <= 4, log <= 3, 2 copies
 WORKLOADS["synthetic"] = (3, 2, 4, 3, 2, 0, ES_LM)
-BASELINE_INDEX = {"cfg1": 0, "cfg2": 1, "synthetic": 4}
-CAPPED = {"cfg1", "cfg2"}          # not exhaustible on one GPU: run until HBM is full
+BASELINE_INDEX = {"cfg1": 0, "cfg2": 1, "cfg3": 2, "cfg4": 3, "synthetic": 4}
+CAPPED = {"cfg1", "cfg2", "cfg3", "cfg4"}  # not exhaustible on one GPU: run until HBM is full
 DEFAULT = "cfg2"
 SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run reports it too)
 # Fingerprint-set size (log2 slots) per workload: ~25-30 % load at the size reached.
 FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30,
-              "cfg2": 31, "cfg1": 31, "synthetic": 33}
+              "cfg2": 31, "cfg1": 31, "cfg3": 31, "cfg4": 30, "synthetic": 33}
 # Bag slots per row for the unbounded-bag configs.  A state d BFS levels below
 # Init holds at most d - 1 distinct messages (every action adds at most one),
 # so this bounds the depth at which the row format -- not memory -- stops the
 # search; a successor that needs more raises RTLA_CAP_ROW, never truncates.
-BAG_CAP = {"cfg2": 18, "cfg1": 24, "synthetic": 12}
+BAG_CAP = {"cfg2": 18, "cfg1": 24, "cfg3": 20, "cfg4": 20, "synthetic": 12}
 # Synthetic microbench: input states per GPU (1e9 over 8 GPUs), the pool half
 # of them are redrawn from (so dedup has hits), states per device batch.
 SYNTH_STATES = 125_000_000
@@ -213,6 +219,7 @@ class Run:
         self.fpl = fpset_log2_for(name, world, args.fpset_log2)
         self.cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=self.fpl, shards=args.shards,
                                bag_cap=BAG_CAP.get(name, 0), frontier_cap=frontier_cap,
+                               symmetry=name in SYMMETRIC,
                                mem_budget=(200 << 30) if args.shards > 1 else 0)
         self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
         self.levels_cap = None   # complete levels a capped search reaches
@@ -456,7 +463,7 @@ def main():
         "invariants": list(inv), "distinct": distinct, "generated": generated, "depth": depth,
         "exhausted": (not run.capped) or bool(run.exhausted), "levels": len(levels),
         "parallelism": "single" if world == 1 else "fp-sharded%d" % world,
-        "fpset_slots_log2": run.fpl, "bag_cap": run.cfg.bag_cap or None,
+        "fpset_slots_log2": run.fpl, "bag_cap": run.cfg.bag_cap or None, "symmetry": run.cfg.symmetry,
         "frontier_arena_rows": info.get("frontier_cap"), "row_bytes": levels[0].row_bytes,
         "rccl_ranks": info.get("world"),
     }
