@@ -74,7 +74,7 @@ enum {
   XF_BLOCK4 = 256,        // compact kernel: 4-wave workgroups instead of 1
   XF_NO_PERSIST = 512,    // compact kernel: one group per wave instead of persistent waves
   XF_CAS_ONLY = 1024,     // compact kernel: probe with CAS only (no load-first)
-  XF_WAVE_KERNEL = 2048,  // use the wave-per-state k_expand (the SYMMETRY path) without symmetry
+  XF_WAVE_KERNEL = 2048,  // use the wave-per-state k_expand (the fallback for rows too wide for the compact tile)
   XF_NO_SPECIAL = 4096,   // compact kernel: run-time layout even for a compiled-in configuration
   XF_DEDUP_ONLY = 8192,   // compact kernel: count new fingerprints, build no rows (synthetic microbench)
 };

@@ -219,6 +219,42 @@ extern "C" int rtla_row_fingerprint(const rtla_cfg* c, const uint32_t* row, uint
   return RTLA_OK;
 }
 
+extern "C" int rtla_orbit_key(const rtla_cfg* c, const uint32_t* row, uint64_t out[2], int* perms) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  FP f{0, 0};
+  switch (L.N) {
+    case 1: f = orbit_key_row<1>(L, row, perms); break;
+    case 2: f = orbit_key_row<2>(L, row, perms); break;
+    case 3: f = orbit_key_row<3>(L, row, perms); break;
+    case 4: f = orbit_key_row<4>(L, row, perms); break;
+    default: f = orbit_key_row<5>(L, row, perms); break;
+  }
+  out[0] = f.a;
+  out[1] = f.b;
+  return RTLA_OK;
+}
+
+extern "C" int rtla_permute_row(const rtla_cfg* c, const uint32_t* row, const int* pi, uint32_t* out) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  int seen = 0;
+  for (int i = 0; i < L.N; i++) {
+    if (pi[i] < 0 || pi[i] >= L.N || (seen >> pi[i] & 1)) return RTLA_E_ARG;
+    seen |= 1 << pi[i];
+  }
+  switch (L.N) {
+    case 1: permute_row<1>(L, row, pi, out); break;
+    case 2: permute_row<2>(L, row, pi, out); break;
+    case 3: permute_row<3>(L, row, pi, out); break;
+    case 4: permute_row<4>(L, row, pi, out); break;
+    default: permute_row<5>(L, row, pi, out); break;
+  }
+  return RTLA_OK;
+}
+
 extern "C" int rtla_state_text(const rtla_cfg* c, const uint32_t* row, char* buf, size_t cap) {
   Layout L;
   int r = layout_from_cfg(c, &L);

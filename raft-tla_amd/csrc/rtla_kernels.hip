@@ -20,8 +20,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "rtla_device.h"
+
 #include "rtla_model.h"
 #include "rtla_synth.h"
 
@@ -30,7 +32,6 @@ using namespace rtla;
 namespace {
 
 constexpr int STAGE_ROWS = 16;  // LDS staging rows per wave
-constexpr int PERM_MAX = 120;   // NMAX! server permutations (symmetry)
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -228,7 +229,7 @@ __device__ __forceinline__ int cover_code(const Layout& L, int inst, int sub) {
 // words so every wave's hash slots stay 8-byte aligned.
 __host__ __device__ constexpr int even_words(int W) { return (W + 1) & ~1; }
 __host__ __device__ constexpr int wave_lds_words(int W) {
-  return (even_words(W) + 32 + 4 * NMAX + STAGE_ROWS * W + 4 * PERM_MAX + 3) & ~3;
+  return (even_words(W) + 32 + 4 * NMAX + STAGE_ROWS * W + 3) & ~3;
 }
 
 // (the readlane builtins return a signed int: widen through uint32_t)
@@ -236,6 +237,33 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return (unsigned long long)lo | (unsigned long long)hi << 32;
+}
+
+// SYMMETRY: orbit key of the successor parent + d (allLogs' fingerprint
+// afp), without materialising it (rtla_model.h sym_key).
+template <int NS, class P>
+__device__ __forceinline__ FP successor_orbit_key(const Layout& L, P prow, const DeltaT<NS>& d, FP afp) {
+  constexpr int EW = 2 + NS;
+  const int ne0 = row_nelec(L, prow);
+  return sym_key<NS>(
+      [&](int i, uint32_t* out) {
+        load_rec<NS>(L, prow, i, out);
+        if (i == d.srv) {
+#pragma unroll
+          for (int w = 0; w < 3 + NS; w++) out[w] = d.rec[w];
+        }
+      },
+      d.nmsg, [&](int q) { return bag_get(L, prow, d, q); }, ne0 + (d.elec ? 1 : 0),
+      [&](int e, uint32_t* out) {
+        if (e < ne0) {
+#pragma unroll
+          for (int w = 0; w < EW; w++) out[w] = prow[L.off_elec + e * EW + w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < EW; w++) out[w] = d.erec[w];
+        }
+      },
+      afp);
 }
 
 // Load the parent row into LDS and derive the per-parent data every lane
@@ -277,27 +305,16 @@ k_expand(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_en
   uint32_t* pall = prow + even_words(W);
   FP* hsrv = reinterpret_cast<FP*>(pall + 32);
   uint32_t* stage = pall + 32 + 4 * NMAX;
-  FP* permfp = reinterpret_cast<FP*>(stage + STAGE_ROWS * W);  // [PERM_MAX]: fp(pi(parent)) + allLogs'
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
 
   unsigned long long my_gen = 0, my_probe = 0;
   const int fixed = L.fam[F_RECEIVE];
-  int nperm = 1;
-#pragma unroll
-  for (int i = 2; i <= NS; i++) nperm *= i;
   for (unsigned long long s = s_begin + (unsigned long long)blockIdx.x * wpb + wave; s < s_end;
        s += (unsigned long long)gridDim.x * wpb) {
     const FP pfp = load_parent<NS>(L, ring_row(cur, s, W), prow, pall, hsrv, lane);
-    if (L.sym) {  // SYMMETRY: per-permutation fingerprints of the parent, lanes over permutations
-      const FP afp = alllogs_fp(L, pall);  // allLogs' is the same for every successor (raft.tla:465)
-      for (int k = lane; k < nperm; k += 64) {
-        int pi[NS], inv[NS];
-        kth_perm<NS>(k, pi, inv);
-        permfp[k] = fp_add(perm_row_fp<NS>(L, prow, pi, inv), afp);
-      }
-      wave_sync();
-    }
+    // SYMMETRY: allLogs' is the same for every successor (raft.tla:465)
+    const FP afp = L.sym ? alllogs_fp(L, pall) : FP{0, 0};
     const int nmsg = row_nmsg(L, prow);
     const int ncand = fixed + 3 * nmsg;
     for (int base = 0; base < ncand; base += 64) {
@@ -321,17 +338,7 @@ k_expand(Layout L, Ring cur, unsigned long long s_begin, unsigned long long s_en
         cfp = fp_add(pfp, delta_fp<NS>(L, prow, d, d.srv >= 0 ? &hsrv[d.srv] : nullptr));
         // seen-set key: the state's own fingerprint, or under SYMMETRY its
         // orbit key (least fingerprint over the server permutations)
-        FP key = cfp;
-        if (L.sym) {
-          key = FP{~0ull, ~0ull};
-          for (int k = 0; k < nperm; k++) {
-            int pi[NS], inv[NS];
-            kth_perm<NS>(k, pi, inv);
-            const FP f = fp_add(permfp[k], perm_delta_fp<NS>(L, prow, d, pi, inv));
-            if (fp_less(f, key)) key = f;
-          }
-          key = orbit_key_finish(key);
-        }
+        const FP key = L.sym ? successor_orbit_key<NS>(L, prow, d, afp) : cfp;
         const int owner = fp_owner(key, box.nshard);
         if (owner == box.me) {
           my_probe++;
@@ -451,11 +458,12 @@ constexpr int NEWCAP = 128; // new-state list (u64 parent records)
 constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
 
 // Per-wave LDS of k_expand_compact (16-byte aligned pieces first):
-// per-state fingerprint with allLogs' applied (GROUP FPs) | per-owner (base,
-// used) of the open outbox chunk | pending new states (NEWCAP parent records)
-// | GROUP rows | allLogs' words of each state | pair ring.
-__host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP) {
-  return (4 * GROUP + 4 * SHARD_MAX + 2 * NEWCAP + GROUP * W + GROUP * AW + RING / 2 + 3) & ~3;
+// per-state fingerprint with allLogs' applied (GROUP FPs) | SYMMETRY: the
+// fingerprint of each state's allLogs' (GROUP FPs) | per-owner (base, used)
+// of the open outbox chunk | pending new states (NEWCAP parent records) |
+// GROUP rows | allLogs' words of each state | pair ring.
+__host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym) {
+  return (4 * GROUP * (sym ? 2 : 1) + 4 * SHARD_MAX + 2 * NEWCAP + GROUP * W + GROUP * AW + RING / 2 + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -526,6 +534,9 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #ifndef RTLA_COMPACT_WAVES_PER_EU
 #define RTLA_COMPACT_WAVES_PER_EU 3  // 166 VGPRs for N = 3 without spills (the default allocation took 170 -> 2 waves)
 #endif
+#ifndef RTLA_SYM_WAVES_PER_EU
+#define RTLA_SYM_WAVES_PER_EU 2      // SYMMETRY: the full Delta and the orbit-key loop stay in VGPRs
+#endif
 // The layout the kernel runs on: the run-time argument, or (LC.N != 0) the
 // configuration compiled in as a template parameter, whose fields the
 // compiler then folds into every offset, bound and loop of the model code.
@@ -560,9 +571,13 @@ __device__ __forceinline__ const Layout& pick_layout(const Layout& rt) {
 
 // GROUP: frontier states per wave-group (64, or 32 for wide rows: halves the
 // LDS tile so more waves fit a CU).  LC: compiled-in layout (Layout{} = use
-// the run-time argument Lrt).
-template <int NS, bool MULTI, int GROUP, Layout LC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTLA_COMPACT_WAVES_PER_EU)))
+// the run-time argument Lrt).  SYM: SYMMETRY Permutations(Server) -- the
+// probe pass evaluates the full Delta of each successor and probes its orbit
+// key (successor_orbit_key) instead of its fingerprint; rows keep the states
+// themselves.
+template <int NS, bool MULTI, int GROUP, Layout LC, bool SYM>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(SYM ? RTLA_SYM_WAVES_PER_EU : RTLA_COMPACT_WAVES_PER_EU)))
 k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long long s_end,
                  unsigned long long cur_base, Ring next, unsigned long long* __restrict__ parents,
                  unsigned long long next_base, unsigned long long next_cap, unsigned long long* table,
@@ -573,9 +588,11 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = L.W, AW = L.all_words;
-  uint32_t* wl = lds + wave * compact_lds_words(W, AW, GROUP);
+  uint32_t* wl = lds + wave * compact_lds_words(W, AW, GROUP, SYM);
   FP* pfpl = reinterpret_cast<FP*>(wl);  // [state lane]: its fingerprint + the allLogs' change (raft.tla:465)
-  unsigned long long* obox = reinterpret_cast<unsigned long long*>(wl + 4 * GROUP);  // [o] base of the open chunk, [SHARD_MAX + o] used
+  FP* afpl = pfpl + GROUP;               // SYM [state lane]: fingerprint of its allLogs'
+  unsigned long long* obox =             // [o] base of the open chunk, [SHARD_MAX + o] used
+      reinterpret_cast<unsigned long long*>(wl + 4 * GROUP * (SYM ? 2 : 1));
   unsigned long long* newl = obox + 2 * SHARD_MAX;
   uint32_t* rows = reinterpret_cast<uint32_t*>(newl + NEWCAP);
   uint32_t* pall = rows + GROUP * W;  // allLogs' words of state lane l: pall[l + w * GROUP]
@@ -797,6 +814,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 #else
       pfpl[lane] = fp_add(row_fp(prow_mine), alllogs_delta<NS>(L, prow_mine, pall_mine));
 #endif
+      if (SYM) afpl[lane] = alllogs_fp(L, pall_mine);
       nmsg = row_nmsg(L, prow_mine);
     }
     wave_sync();
@@ -846,7 +864,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 #else
         const FP qfp = pfpl[sl];
 #endif
-        DeltaFpT<NS> d;
+        std::conditional_t<SYM, DeltaT<NS>, DeltaFpT<NS>> d;
         d.enabled = 0;
         if (!(xflags & XF_NO_DELTA)) {
           const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
@@ -879,16 +897,22 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         FP cf{0, 0};
         int owner = me;
         if (en && d.in_model) {
-          const FP cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
-                                                : fp_add(qfp, delta_fp<NS>(L, prow, d));
+          FP cfp;
+          if constexpr (SYM) cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
+          else
+            cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
+                                        : fp_add(qfp, delta_fp<NS>(L, prow, d));
 #ifndef RTLA_PFP_SHFL
           const FP qfp0 = row_fp(prow);
 #endif
           if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
+            // seen-set key: the fingerprint, or under SYMMETRY the orbit key
+            FP key = cfp;
+            if constexpr (SYM) key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
             probe = !(xflags & XF_NO_PROBE);
-            cf = cfp;
-            idx = cfp.a >> (64 - tlog2);
-            owner = MULTI ? fp_owner(cfp, box.nshard) : me;
+            cf = key;
+            idx = key.a >> (64 - tlog2);
+            owner = MULTI ? fp_owner(key, box.nshard) : me;
           }
         }
         if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
@@ -1278,8 +1302,11 @@ int expand_lane_wpb(const Layout& L) {
 #ifndef RTLA_GROUP64_LDS
 #define RTLA_GROUP64_LDS (16 * 1024)
 #endif
+// SYMMETRY: always 32 (one instantiation per N; the orbit-key arithmetic,
+// not the tile, bounds that kernel).
 constexpr int compact_group(const Layout& L) {
-  return compact_lds_words(L.W, L.all_words, 64) * sizeof(uint32_t) <= RTLA_GROUP64_LDS ? 64 : 32;
+  if (L.sym) return 32;
+  return compact_lds_words(L.W, L.all_words, 64, false) * sizeof(uint32_t) <= RTLA_GROUP64_LDS ? 64 : 32;
 }
 
 static int device_cus() {
@@ -1295,7 +1322,7 @@ static int device_cus() {
 
 
 int expand_compact_wpb(const Layout& L) {
-  const size_t per = (size_t)compact_lds_words(L.W, L.all_words, compact_group(L)) * sizeof(uint32_t);
+  const size_t per = (size_t)compact_lds_words(L.W, L.all_words, compact_group(L), L.sym) * sizeof(uint32_t);
   // one wave may use up to the CU's 160 KiB of LDS; instance ids fit 8 bits per 64-instance window
   if (per > 160 * 1024 || ((L.fam[F_COUNT] + 63) / 64) * 64 > 256) return 0;
   return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
@@ -1326,15 +1353,15 @@ constexpr Layout EXHAUST = layout_of(3, 2, 2, 2, 1, 2, 3, 3, INV_ELECTION_SAFETY
 static_assert(CFG2.N == 3 && CFG1.N == 3 && EXHAUST.N == 3, "compiled-in layouts must be valid");
 }  // namespace specs
 
-template <int NS, int GROUP, Layout LC>
+template <int NS, int GROUP, Layout LC, bool SYM = false>
 static hipError_t launch_compact(const Layout& L, bool multi, const Ring& cur, uint64_t s_begin, uint64_t s_end,
                                  uint64_t cur_base, const Ring& next, uint64_t* parents, uint64_t next_base,
                                  uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
                                  hipStream_t st, int xflags, uint64_t* sent, int wpb) {
-  auto kfn = multi ? k_expand_compact<NS, true, GROUP, LC> : k_expand_compact<NS, false, GROUP, LC>;
+  auto kfn = multi ? k_expand_compact<NS, true, GROUP, LC, SYM> : k_expand_compact<NS, false, GROUP, LC, SYM>;
   const uint64_t groups = (s_end - s_begin + GROUP - 1) / GROUP;
   uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
-  const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words, GROUP) * sizeof(uint32_t);
+  const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words, GROUP, SYM) * sizeof(uint32_t);
   if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
     static int per_cu[2][2];  // per instantiation: [multi][one-wave blocks]
     int& pc = per_cu[multi][wpb == 1];
@@ -1361,7 +1388,7 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
                          uint64_t* sent, hipEvent_t mid) {
   if (s_end <= s_begin) return hipSuccess;
   const int cwpb = expand_compact_wpb(L);
-  if (cwpb > 0 && !L.sym && !(xflags & XF_WAVE_KERNEL) && (box.nshard == 1 || sent)) {
+  if (cwpb > 0 && !(xflags & XF_WAVE_KERNEL) && (box.nshard == 1 || sent)) {
     const bool multi = box.nshard > 1;
     const int wpb = (xflags & XF_BLOCK4) ? cwpb : 1;  // one-wave workgroups by default
     hipError_t e = hipSuccess;
@@ -1373,7 +1400,20 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
     done = true;                                                                                   \
   }
     bool done = false;
-    if (!(xflags & XF_NO_SPECIAL)) {
+    if (L.sym) {
+#define RTLA_SYMN(n) \
+  case n: e = launch_compact<n, 32, Layout{}, true>(RTLA_ARGS); break;
+      switch (L.N) {
+        RTLA_SYMN(1)
+        RTLA_SYMN(2)
+        RTLA_SYMN(3)
+        RTLA_SYMN(4)
+        default: RTLA_SYMN(5)
+      }
+#undef RTLA_SYMN
+      done = true;
+    }
+    if (!done && !(xflags & XF_NO_SPECIAL)) {
       RTLA_SPEC(CFG2)
       RTLA_SPEC(CFG1)
       RTLA_SPEC(EXHAUST)
@@ -1400,8 +1440,8 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
     }
     return hipGetLastError();
   }
-  // one wave per state: SYMMETRY (the orbit key needs the full Delta of each
-  // successor), or rows too wide for the compacting kernel's LDS tile
+  // one wave per state: rows too wide for the compacting kernel's LDS tile
+  // (or forced, XF_WAVE_KERNEL)
   RTLA_DISPATCH_N(L, k_expand, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, cur,
                   (unsigned long long)s_begin, (unsigned long long)s_end, (unsigned long long)cur_base, next,
                   (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap,

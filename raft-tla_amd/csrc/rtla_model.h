@@ -881,18 +881,30 @@ RTLA_HD void materialize(const Layout& L, P row, const DeltaT<NR>& d, R all_new,
 
 // ------------------------------------------------------------ symmetry ----
 // SYMMETRY Permutations(Server) (specs/MC.tla).  TLC identifies a state with
-// its server-permuted images.  The dedup key of a successor is the least
-// (a, b) over all N! permutations pi of the fingerprint of pi(state): record
-// i moves to position pi[i] and every server-valued field is relabelled
-// (votedFor, votesResponded/Granted, voterLog and next/matchIndex domains,
-// msource/mdest, eleader, evotes, evoterLog).  The fingerprint being a sum
-// of per-component hashes, fp(pi(child)) = fp(pi(parent)) + the relabelled
-// hashes of the few components the action changes: the kernel computes the
-// N! parent values once per frontier state and then pays, per successor and
-// permutation, two server-record hashes, two per bag-slot write and one per
-// new election record.  The row keeps the state itself (and its own
-// fingerprint): TLC explores the state it generated, and the orbit key is
-// used only for the seen set and shard ownership.
+// its server-permuted images: a successor is new iff its orbit was not seen.
+// The seen-set key of a state s is a function of its orbit only:
+//
+//   key(s) = finish( min over pi in C(s) of fp(pi(s)) ) + fp(allLogs)
+//
+// where pi(s) moves server record i to position pi[i] and relabels every
+// server-valued field (votedFor, votesResponded/Granted, voterLog and
+// next/matchIndex domains, msource/mdest, eleader, evotes, evoterLog), and
+// C(s) is the set of permutations that sort the servers by a signature:
+// sig_i(s) is a hash of everything server i "sees" with server names folded
+// to self/other (its record, and the multisets of messages it sent and is
+// sent), so sig_{pi[i]}(pi(s)) = sig_i(s) for every pi.  C(s) = { pi :
+// sig_i < sig_j => pi[i] < pi[j] }; for s' = rho(s), C(s') = C(s) o rho^-1,
+// so { pi(s') : pi in C(s') } = { pi(s) : pi in C(s) } and the key is
+// orbit-invariant -- whatever the signature's quality.  A good signature only
+// makes C small: servers tie only when they look alike, and then all |C| =
+// prod(tie-group sizes)! orderings are tried.  (TLC itself fingerprints all
+// N! images of every successor.)  allLogs holds no server names.
+//
+// The row keeps the state itself (and its own fingerprint): TLC explores the
+// state it generated; the orbit key is used for the seen set and shard
+// ownership only.  The same sym_key template runs in the kernels (on a parent
+// row patched by a Delta, never materialised) and on the host (rows), so the
+// keys agree everywhere.
 
 // k-th permutation of 0..N-1 in lexicographic order (Lehmer code)
 template <int NS>
@@ -937,15 +949,19 @@ RTLA_HD uint32_t sel_word(const uint32_t* a, int i) {  // a[i] for a run-time i,
     if (k == i) r = a[k];
   return r;
 }
+template <int NS>
+RTLA_HD uint32_t perm_id(uint32_t v, const int* pi) {  // a server id (or NIL) relabelled
+  uint32_t r = v;
+#pragma unroll
+  for (int j = 0; j < NS; j++)
+    if (v == (uint32_t)j) r = (uint32_t)pi[j];
+  return r;
+}
 // server record relabelled by pi (the record of server i, now at pi[i])
 template <int NS>
 RTLA_HD void perm_srv_rec(const uint32_t* rec, const int* pi, const int* inv, uint32_t* out) {
-  const uint32_t w0 = rec[0], vf = s_voted(w0);
-  uint32_t vfp = vf;
-#pragma unroll
-  for (int j = 0; j < NS; j++)
-    if (vf == (uint32_t)j) vfp = (uint32_t)pi[j];
-  out[0] = s_make(s_term(w0), s_role(w0), vfp, s_commit(w0), perm_mask<NS>(s_vresp(w0), pi),
+  const uint32_t w0 = rec[0];
+  out[0] = s_make(s_term(w0), s_role(w0), perm_id<NS>(s_voted(w0), pi), s_commit(w0), perm_mask<NS>(s_vresp(w0), pi),
                   perm_mask<NS>(s_vgrant(w0), pi), perm_mask<NS>(s_vlp(w0), pi));
   out[1] = rec[1];
   uint32_t nm = 0;
@@ -963,23 +979,13 @@ RTLA_HD void perm_srv_rec(const uint32_t* rec, const int* pi, const int* inv, ui
 template <int NS>
 RTLA_HD uint64_t perm_msg_slot(uint64_t v, const int* pi) {  // msource bits 2-4, mdest bits 5-7
   if (!v) return 0;  // empty slot (h_msg(0) = 0)
-  const uint32_t src = m_src(v), dst = m_dst(v);
-  uint32_t ps = src, pd = dst;
-#pragma unroll
-  for (int j = 0; j < NS; j++) {
-    if (src == (uint32_t)j) ps = (uint32_t)pi[j];
-    if (dst == (uint32_t)j) pd = (uint32_t)pi[j];
-  }
-  return (v & ~(63ull << 2)) | (uint64_t)ps << 2 | (uint64_t)pd << 5;
+  return (v & ~(63ull << 2)) | (uint64_t)perm_id<NS>(m_src(v), pi) << 2 | (uint64_t)perm_id<NS>(m_dst(v), pi) << 5;
 }
 template <int NS>
 RTLA_HD void perm_elec(const uint32_t* e, const int* pi, const int* inv, uint32_t* out) {
-  const uint32_t w0 = e[0], ld = (w0 >> 4) & 7u;
-  uint32_t pl = ld;
-#pragma unroll
-  for (int j = 0; j < NS; j++)
-    if (ld == (uint32_t)j) pl = (uint32_t)pi[j];
-  out[0] = (w0 & 15u) | pl << 4 | perm_mask<NS>((w0 >> 7) & 31u, pi) << 7 | perm_mask<NS>((w0 >> 12) & 31u, pi) << 12;
+  const uint32_t w0 = e[0];
+  out[0] = (w0 & 15u) | perm_id<NS>((w0 >> 4) & 7u, pi) << 4 | perm_mask<NS>((w0 >> 7) & 31u, pi) << 7 |
+           perm_mask<NS>((w0 >> 12) & 31u, pi) << 12;
   out[1] = e[1];
   uint32_t vl[NS];
 #pragma unroll
@@ -988,88 +994,170 @@ RTLA_HD void perm_elec(const uint32_t* e, const int* pi, const int* inv, uint32_
   for (int k = 0; k < NS; k++) out[2 + k] = sel_word<NS>(vl, inv[k]);
 }
 
-// Fingerprint of pi(row) without its allLogs part (permutation-free):
-// N server records, the bag and the election records, relabelled.
-template <int NS, class P>
-RTLA_HD FP perm_row_fp(const Layout& L, P row, const int* pi, const int* inv) {
-  constexpr int SW = 3 + NS, EW = 2 + NS;
-  FP f{0, 0};
-#pragma unroll
-  for (int i = 0; i < NS; i++) {
-    uint32_t rec[SW], out[SW];
-    load_rec<NS>(L, row, i, rec);
-    perm_srv_rec<NS>(rec, pi, inv, out);
-    f = fp_add(f, h_srv(pi[i], out, SW));
-  }
-  const int nm = row_nmsg(L, row), ne = row_nelec(L, row);
-  for (int q = 0; q < nm; q++) f = fp_add(f, h_msg(perm_msg_slot<NS>(bag_slot(L, row, q), pi)));
-  for (int e = 0; e < ne; e++) {
-    uint32_t er[EW], out[EW];
-#pragma unroll
-    for (int w = 0; w < EW; w++) er[w] = row[L.off_elec + e * EW + w];
-    perm_elec<NS>(er, pi, inv, out);
-    f = fp_add(f, h_elec(out, EW));
-  }
-  return f;
+RTLA_HD uint32_t mix32(uint32_t x) {  // lowbias32 finalizer (signatures only)
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
 }
 
-// fp(pi(row + d)) - fp(pi(row)): only the components the delta changes
-// (one server record, <= 3 bag slots, one appended election record).
-template <int NS, class P, int NR>
-RTLA_HD FP perm_delta_fp(const Layout& L, P row, const DeltaT<NR>& d, const int* pi, const int* inv) {
-  constexpr int SW = 3 + NS, EW = 2 + NS;
-  FP f{0, 0};
-  if (d.srv >= 0) {
-    uint32_t rec[SW], out[SW];
-    load_rec<NS>(L, row, d.srv, rec);
-    int to = 0;
+// Local part of server i's signature: its record with server names folded
+// to self / other / Nil; the other servers' entries (vote bits, voterLog,
+// next/matchIndex) enter as an order-free sum.
+template <int NS>
+RTLA_HD uint32_t srv_sig(int i, const uint32_t* rec) {
+  const uint32_t w0 = rec[0], nm = rec[2];
+  const uint32_t vf = s_voted(w0), vr = s_vresp(w0), vg = s_vgrant(w0), vl = s_vlp(w0);
+  uint32_t h = mix32(s_term(w0) | s_role(w0) << 4 | s_commit(w0) << 8 |
+                     (vf == NIL ? 0u : vf == (uint32_t)i ? 1u : 2u) << 12);
+  h = mix32(h ^ rec[1]);
+  uint32_t others = 0;
 #pragma unroll
-    for (int j = 0; j < NS; j++)
-      if (j == d.srv) to = pi[j];
-    perm_srv_rec<NS>(rec, pi, inv, out);
-    f = fp_sub(f, h_srv(to, out, SW));
-    perm_srv_rec<NS>(d.rec, pi, inv, out);
-    f = fp_add(f, h_srv(to, out, SW));
+  for (int j = 0; j < NS; j++) {
+    const uint32_t t = (vr >> j & 1u) | (vg >> j & 1u) << 1 | (vl >> j & 1u) << 2 | (vf == (uint32_t)j ? 8u : 0u) |
+                       nm_next(nm, j) << 4 | nm_match(nm, j) << 8;
+    const uint32_t x = mix32(t ^ mix32(rec[3 + j] + 0x9e3779b9u));
+    if (j == i) h = mix32(h ^ x);
+    else others += x;
   }
+  return mix32(h ^ mix32(others + 0x85ebca6bu));
+}
+
+// First hash state of a record hashed at position p (run-time p < NS):
+// hash_words' tag mixing of TAG_SRV << 8 | p, folded to constants.
+template <int NS>
+RTLA_HD FP srv_seed(int p) {
+  FP s{0, 0};
 #pragma unroll
-  for (int q = 0; q < 3; q++)
-    if (q < d.nops)
-      f = fp_add(f, fp_sub(h_msg(perm_msg_slot<NS>(d.op_new[q], pi)), h_msg(perm_msg_slot<NS>(d.op_old[q], pi))));
-  if (d.elec) {
-    uint32_t out[EW];
-    perm_elec<NS>(d.erec, pi, inv, out);
-    f = fp_add(f, h_elec(out, EW));
+  for (int k = 0; k < NS; k++) {
+    const uint64_t tag = (uint64_t)(TAG_SRV << 8 | k);
+    if (k == p) {
+      s.a = mix_a(tag * 0x9E3779B97F4A7C15ull + 0x243f6a8885a308d3ull);
+      s.b = mix_b(tag * 0xD1B54A32D192ED03ull + 0x13198a2e03707344ull);
+    }
   }
-  return f;
+  return s;
+}
+template <int N>
+RTLA_HD FP hash_words_from(FP s, const uint32_t* w) {  // = hash_words(tag, w, N) given its seed s
+#pragma unroll
+  for (int k = 0; k < N; k += 2) {
+    const uint64_t x = (uint64_t)w[k] | ((k + 1 < N) ? (uint64_t)w[k + 1] << 32 : 0ull);
+    s.a = mix_a(s.a ^ x);
+    s.b = mix_b(s.b + x);
+  }
+  return s;
 }
 
 RTLA_HD bool fp_less(FP x, FP y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }
 
-// The least of N! fingerprints is skewed towards 0 (density N!(1-x)^(N!-1)),
-// which would pile the orbit keys into the low slots of the open-addressing
-// set.  Re-mix it with a bijection of the 128 bits (mix_b and mix_a are
-// bijective; a' depends on b only through an xor) so home slots and shard
-// ownership are uniform again and no two orbit keys merge.
+// The least of several fingerprints is skewed towards 0, which would pile
+// the orbit keys into the low slots of the open-addressing set.  Re-mix it
+// with a bijection of the 128 bits (mix_b and mix_a are bijective; a'
+// depends on b only through an xor) so home slots and shard ownership are
+// uniform again and no two orbit keys merge.
 RTLA_HD FP orbit_key_finish(FP m) {
   return FP{mix_a(m.a ^ (m.b >> 29 | m.b << 35)), mix_b(m.b)};
 }
 
-// Orbit key of a row from scratch: least fingerprint over all N! server
-// permutations (host: Init and tests; the kernels derive it per successor
-// from per-permutation parent fingerprints, k_expand).
-template <int NS, class P>
-RTLA_HD FP orbit_key(const Layout& L, P row, FP all_fp) {
-  int nperm = 1;
+// The orbit key of a state given through accessors:
+//   rec_of(i, out)  server i's record (3 + NS words)
+//   slot_of(q)      bag slot q < nmsg (0 = empty)
+//   elec_of(e, out) election record e < nelec (2 + NS words)
+//   afp             fingerprint of allLogs (permutation-free)
+// `perms` (optional) receives |C(s)|.
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD FP sym_key(RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp, int* perms = nullptr) {
+  constexpr int SW = 3 + NS, EW = 2 + NS;
+  // signatures: local part (high half) | sent/received message multisets
+  uint32_t ms[NS], mr[NS];
+  uint64_t sig[NS];
 #pragma unroll
-  for (int i = 2; i <= NS; i++) nperm *= i;
+  for (int j = 0; j < NS; j++) ms[j] = mr[j] = 0;
+  for (int q = 0; q < nmsg; q++) {
+    const uint64_t v = slot_of(q);
+    if (!v) continue;
+    const uint32_t src = m_src(v), dst = m_dst(v);
+    const uint64_t anon = v & ~(63ull << 2);  // names dropped (msource /= mdest in every message)
+    const uint32_t c = mix32((uint32_t)anon ^ mix32((uint32_t)(anon >> 32) + 0x632be5abu));
+    const uint32_t cr = mix32(c ^ 0x5bd1e995u);
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      ms[j] += src == (uint32_t)j ? c : 0u;
+      mr[j] += dst == (uint32_t)j ? cr : 0u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
+    uint32_t rec[SW];
+    rec_of(i, rec);
+    sig[i] = (uint64_t)srv_sig<NS>(i, rec) << 32 | mix32(ms[i] ^ mix32(mr[i] + 0x27d4eb2fu));
+  }
+  // pi[i] ranges over [lo_i, lo_i + cnt_i); server i picks among the
+  // positions its tie group has left: rad_i = cnt_i - (tied servers before i)
+  int lo[NS], cnt[NS], rad[NS];
+  int ncomb = 1;
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
+    int l = 0, c = 0, b = 0;
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      l += sig[j] < sig[i] ? 1 : 0;
+      c += sig[j] == sig[i] ? 1 : 0;
+      if (j < i) b += sig[j] == sig[i] ? 1 : 0;
+    }
+    lo[i] = l;
+    cnt[i] = c;
+    rad[i] = c - b;
+    ncomb *= c - b;
+  }
+  if (perms) *perms = ncomb;
   FP best{~0ull, ~0ull};
-  for (int k = 0; k < nperm; k++) {
+  for (int k = 0; k < ncomb; k++) {
     int pi[NS], inv[NS];
-    kth_perm<NS>(k, pi, inv);
-    const FP f = fp_add(perm_row_fp<NS>(L, row, pi, inv), all_fp);
+    uint32_t used = 0;
+    int rem = k;
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+      int dgt = 0;
+      if (rad[i] > 1) {
+        dgt = rem % rad[i];
+        rem /= rad[i];
+      }
+      const uint32_t free = ((1u << cnt[i]) - 1u) << lo[i] & ~used;
+      int p = 0, c = dgt;
+#pragma unroll
+      for (int b = 0; b < NS; b++)
+        if (free >> b & 1u) {
+          if (c == 0) p = b;
+          c--;
+        }
+      pi[i] = p;
+      used |= 1u << p;
+    }
+#pragma unroll
+    for (int i = 0; i < NS; i++)
+#pragma unroll
+      for (int j = 0; j < NS; j++)
+        if (pi[j] == i) inv[i] = j;
+    FP f{0, 0};
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+      uint32_t rec[SW], out[SW];
+      rec_of(i, rec);
+      perm_srv_rec<NS>(rec, pi, inv, out);
+      f = fp_add(f, hash_words_from<SW>(srv_seed<NS>(pi[i]), out));
+    }
+    for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot<NS>(slot_of(q), pi)));
+    for (int e = 0; e < nelec; e++) {
+      uint32_t er[EW], out[EW];
+      elec_of(e, er);
+      perm_elec<NS>(er, pi, inv, out);
+      f = fp_add(f, h_elec(out, EW));
+    }
     if (fp_less(f, best)) best = f;
   }
-  return orbit_key_finish(best);
+  return fp_add(orbit_key_finish(best), afp);
 }
 
 // allLogs part of a fingerprint: sum of h_all over the set bits of the words
@@ -1085,6 +1173,50 @@ RTLA_HD FP alllogs_fp(const Layout& L, Q words) {
     }
   }
   return f;
+}
+
+// Orbit key of a materialised row (host: rtla_orbit_key, tests).
+template <int NS, class P>
+RTLA_HD FP orbit_key_row(const Layout& L, P row, int* perms = nullptr) {
+  constexpr int EW = 2 + NS;
+  return sym_key<NS>([&](int i, uint32_t* out) { load_rec<NS>(L, row, i, out); }, row_nmsg(L, row),
+                     [&](int q) { return bag_slot(L, row, q); }, row_nelec(L, row),
+                     [&](int e, uint32_t* out) {
+                       for (int w = 0; w < EW; w++) out[w] = row[L.off_elec + e * EW + w];
+                     },
+                     alllogs_fp(L, row + L.off_all), perms);
+}
+
+// pi(row): the server-permuted image of a row, with its own fingerprint
+// (host: rtla_permute_row, the symmetry tests).  Bag slots and election
+// records keep their order (both are multisets in the fingerprint).
+template <int NS, class P, class Q>
+RTLA_HD void permute_row(const Layout& L, P row, const int* pi, Q out) {
+  constexpr int SW = 3 + NS, EW = 2 + NS;
+  int inv[NS];
+  for (int i = 0; i < NS; i++)
+    for (int j = 0; j < NS; j++)
+      if (pi[j] == i) inv[i] = j;
+  for (int w = 0; w < L.W; w++) out[w] = row[w];
+  for (int i = 0; i < NS; i++) {
+    uint32_t rec[SW], img[SW];
+    load_rec<NS>(L, row, i, rec);
+    perm_srv_rec<NS>(rec, pi, inv, img);
+    for (int w = 0; w < SW; w++) out[L.off_srv + pi[i] * SW + w] = img[w];
+  }
+  const int nm = row_nmsg(L, row), ne = row_nelec(L, row);
+  for (int q = 0; q < nm; q++) {
+    const uint64_t v = perm_msg_slot<NS>(bag_slot(L, row, q), pi);
+    out[L.off_bag + 2 * q] = (uint32_t)v;
+    out[L.off_bag + 2 * q + 1] = (uint32_t)(v >> 32);
+  }
+  for (int e = 0; e < ne; e++) {
+    uint32_t er[EW], img[EW];
+    for (int w = 0; w < EW; w++) er[w] = row[L.off_elec + e * EW + w];
+    perm_elec<NS>(er, pi, inv, img);
+    for (int w = 0; w < EW; w++) out[L.off_elec + e * EW + w] = img[w];
+  }
+  row_set_fp(out, row_fingerprint(L, out));
 }
 
 // ---------------------------------------------------------- invariants ----

@@ -97,6 +97,8 @@ def _load():
         "rtla_probe_bench": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_uint64)]),
         "rtla_random_rows": (C.c_int, [P(_Cfg), C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, P(C.c_uint32)]),
         "rtla_synthetic_step": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, P(_Stats)]),
+        "rtla_orbit_key": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_uint64), P(C.c_int)]),
+        "rtla_permute_row": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_int), P(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -111,7 +113,8 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_trace", "rtla_frontier", "rtla_coverage", "rtla_device_info", "rtla_row_words", "rtla_init_row",
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
-            "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step"]
+            "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step",
+            "rtla_orbit_key", "rtla_permute_row"]
 
 SYNTH_SEED = 0x5AF72025  # the synthetic microbench's PRNG seed
 
@@ -227,6 +230,27 @@ def row_fingerprint(cfg: Config, row: Sequence[int]):
     out = (C.c_uint64 * 2)()
     _check(_lib.rtla_row_fingerprint(C.byref(cc), arr, out), "rtla_row_fingerprint")
     return out[0], out[1]
+
+
+def orbit_key(cfg: Config, row: Sequence[int]):
+    """SYMMETRY seen-set key of the row's orbit and the number of permutation
+    images it compared (rtla_model.h sym_key; host)."""
+    cc = cfg.c()
+    arr = (C.c_uint32 * len(row))(*row)
+    out = (C.c_uint64 * 2)()
+    n = C.c_int(0)
+    _check(_lib.rtla_orbit_key(C.byref(cc), arr, out, C.byref(n)), "rtla_orbit_key")
+    return (out[0], out[1]), n.value
+
+
+def permute_row(cfg: Config, row: Sequence[int], pi: Sequence[int]):
+    """The server-permuted image of a row (server i moved to pi[i])."""
+    cc = cfg.c()
+    arr = (C.c_uint32 * len(row))(*row)
+    p = (C.c_int * len(pi))(*pi)
+    out = (C.c_uint32 * len(row))()
+    _check(_lib.rtla_permute_row(C.byref(cc), arr, p, out), "rtla_permute_row")
+    return list(out)
 
 
 def stored_fingerprint(row: Sequence[int]):

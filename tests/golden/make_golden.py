@@ -53,6 +53,13 @@ PREFIXES = {
     "n3_v2_t3_l2_c1_prefix": (3, 2, 3, 2, 1, 0, (ES, LM), 25_000_000),
     "n3_v1_t2_l1_c1_prefix": (3, 1, 2, 1, 1, 0, (NTL,), 30_000_000),
 }
+# SYMMETRY prefixes (orbit counts per level; no text hashes: the orbit
+# representatives kept differ between implementations).  N = 4 and BASELINE
+# configs[3] (N = 5) as stated.
+SYM_PREFIXES = {
+    "n4_v1_t2_l1_m1_sym_prefix": (4, 1, 2, 1, 1, 1, (NTL,), 3_000_000),
+    "n5_v1_t3_l2_c1_sym_prefix": (5, 1, 3, 2, 1, 0, (), 3_000_000),
+}
 
 
 def main():
@@ -111,6 +118,18 @@ def main():
                      "distinct": r["distinct"], "generated": r["generated"], "max_msgs_seen": r["max_msgs"],
                      "level_text_hash": ["%016x" % h for h in r["level_text_hash"]],
                      "source": "oracle/raft_cpu.c, first %d complete levels" % len(r["levels"])}
+        print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
+    for name, (n, v, t, l, c, m, inv, cap) in SYM_PREFIXES.items():
+        if not big or (only and name not in only):
+            continue
+        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap, symmetry=True)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8)
+        assert r["rc"] in (0, -4), (name, r["rc"])
+        out[name] = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
+                     "invariants": list(inv), "prefix": True, "symmetry": True, "levels": r["levels"],
+                     "distinct": r["distinct"], "generated": r["generated"], "max_msgs_seen": r["max_msgs"],
+                     "source": "oracle/raft_cpu.c (orbit key: least serialisation over server permutations), "
+                               "first %d complete levels" % len(r["levels"])}
         print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)

@@ -187,7 +187,7 @@ def test_full_size_counts_match_golden(name):
 
 # bench.py's row formats (bag slots) for the prefix models: the same layouts
 # the bench runs, i.e. the kernels compiled for them (rtla_kernels.hip specs)
-PREFIX_BAG = {"n3_v2_t3_l2_c1_prefix": 18, "n3_v1_t2_l1_c1_prefix": 24}
+PREFIX_BAG = {"n3_v2_t3_l2_c1_prefix": 18, "n3_v1_t2_l1_c1_prefix": 24, "n5_v1_t3_l2_c1_sym_prefix": 20}
 
 
 def level_text_hash(cfg, rows):
@@ -372,9 +372,11 @@ def test_recover_rejects_other_configuration(tmp_path):
 
 # ---- SYMMETRY Permutations(Server) (specs/MC.tla Perms) ----
 # The golden orbit counts come from the C oracle (least serialisation over
-# server permutations) and, for N=2, the value oracle's orbit BFS; the GPU
-# keys the seen set by the least FINGERPRINT over permutations instead, so
-# agreement checks the orbit relation, not a shared implementation.
+# all server permutations) and, for N=2, the value oracle's orbit BFS; the
+# GPU keys the seen set by the least fingerprint over the permutations that
+# sort the servers by signature (rtla_model.h sym_key), so agreement checks
+# the orbit relation, not a shared implementation.  N = 4 and N = 5
+# (BASELINE configs[3]) are covered by the prefix fixtures above.
 SYM_SMALL = sorted(k for k in SMALL if GOLD[k].get("symmetry"))
 
 
@@ -425,14 +427,17 @@ def test_symmetry_stored_rows_are_generated_states():
             assert len({rtla.state_text(cfg, r) for r in rows}) == len(rows)
 
 
-def test_wave_kernel_without_symmetry_matches_golden():
-    """The wave-per-state k_expand (the symmetry path) on plain models, forced
-    with RTLA_XFLAGS=2048 in a child process (the flag is read once)."""
+@pytest.mark.parametrize("name", ["n2_v2_t3_l2_m1", "n3_v1_t2_l1_m1_sym"])
+def test_wave_kernel_matches_golden(name):
+    """The wave-per-state k_expand (the fallback for rows too wide for the
+    compacting kernel), forced with RTLA_XFLAGS=2048 in a child process (the
+    flag is read once), with and without symmetry."""
     import subprocess
     import sys
-    code = ("import json, rtla, sys; g = json.load(open(sys.argv[1]))['n2_v2_t3_l2_m1'];"
+    code = ("import json, rtla, sys; g = json.load(open(sys.argv[1]))[sys.argv[2]];"
             "r = rtla.check(rtla.Config(g['n_server'], g['n_value'], g['max_term'], g['max_log'], g['max_copies'],"
-            " g['max_msgs'], tuple(g['invariants']), fpset_log2=20, mem_budget=1 << 30), trace=False);"
+            " g['max_msgs'], tuple(g['invariants']), fpset_log2=22, mem_budget=1 << 30,"
+            " symmetry=g.get('symmetry', False)), trace=False);"
             "assert [[lv.new, lv.generated] for lv in r.levels] == g['levels'], 'levels differ';"
             "assert (r.distinct, r.generated, r.depth) == (g['distinct'], g['generated'], g['depth']);"
             "print('ok', r.distinct)")
@@ -440,7 +445,7 @@ def test_wave_kernel_without_symmetry_matches_golden():
                PYTHONPATH=os.pathsep.join([os.path.join(os.path.dirname(__file__), "..", "raft-tla_amd"),
                                            os.environ.get("PYTHONPATH", "")]))
     out = subprocess.run([sys.executable, "-c", code, os.path.join(os.path.dirname(__file__), "golden",
-                                                                   "bfs_counts.json")],
+                                                                   "bfs_counts.json"), name],
                          env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
 

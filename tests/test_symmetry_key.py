@@ -1,0 +1,81 @@
+"""The SYMMETRY orbit key on the CPU (rtla_model.h sym_key through
+rtla_orbit_key / rtla_permute_row): every server permutation of a state has
+its state's key, and two states share a key exactly when some permutation
+maps one onto the other (checked against the least TLC text over all
+permutations, the value oracle's notion of an orbit).  The states are the
+synthetic microbench's random rows (few ties between servers), copies of
+them with servers made look-alike and the bag emptied (many ties: the
+signature-pruned search must then try every ordering of the tied servers),
+and Init (all servers alike).  The GPU side -- orbit counts of whole BFS runs
+against the C oracle -- is in test_gpu.py."""
+import itertools
+import random
+
+import pytest
+
+import rtla
+
+OFF_SRV, OFF_HDR = 5, 4  # rtla_model.h make_layout
+
+
+def cfg_of(n):
+    t, l = (3, 2) if n <= 3 else (2, 1)
+    return rtla.Config(n_server=n, n_value=1, max_term=t, max_log=l, max_copies=1, max_msgs=0,
+                       invariants=(), bag_cap=12, symmetry=True)
+
+
+def look_alike(cfg, row, k):
+    """Servers 1..k take server 0's record relabelled into their place (the
+    image of record 0 under the transposition (0 i)); the bag is emptied."""
+    n, sw = cfg.n_server, 3 + cfg.n_server
+    out = list(row)
+    for i in range(1, k + 1):
+        pi = list(range(n))
+        pi[0], pi[i] = i, 0
+        img = rtla.permute_row(cfg, row, pi)
+        out[OFF_SRV + i * sw:OFF_SRV + (i + 1) * sw] = img[OFF_SRV + i * sw:OFF_SRV + (i + 1) * sw]
+    out[OFF_HDR] &= ~0xFF
+    return out
+
+
+def min_text(cfg, row, perms):
+    return min(rtla.state_text(cfg, rtla.permute_row(cfg, row, pi)) for pi in perms)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5])
+def test_orbit_key_is_a_function_of_the_orbit(n):
+    cfg = cfg_of(n)
+    all_perms = [list(p) for p in itertools.permutations(range(n))]
+    rng = random.Random(n)
+    base = rtla.random_rows(cfg, 0, 40 if n < 5 else 16, pool=0)
+    rows = base + [look_alike(cfg, r, rng.randrange(1, n)) for r in base[:12]] + [rtla.init_row(cfg)]
+    # permuted copies: equal orbits under different names
+    rows += [rtla.permute_row(cfg, r, rng.choice(all_perms)) for r in rows[:20]]
+    keys, orbits, nperm = [], [], []
+    for r in rows:
+        key, c = rtla.orbit_key(cfg, r)
+        nperm.append(c)
+        for pi in (all_perms if n <= 4 else rng.sample(all_perms, 12)):
+            assert rtla.orbit_key(cfg, rtla.permute_row(cfg, r, pi))[0] == key
+        keys.append(key)
+        orbits.append(min_text(cfg, r, all_perms))
+    # same key <=> same orbit
+    by_key = {}
+    for k, o in zip(keys, orbits):
+        by_key.setdefault(k, set()).add(o)
+    assert all(len(v) == 1 for v in by_key.values())
+    assert len(by_key) == len(set(orbits))
+    # Init: every server alike -> all N! orderings compared; random states: mostly one
+    assert nperm[len(base) + 12] == len(all_perms)
+    assert sum(nperm[:len(base)]) <= 1.5 * len(base), nperm[:len(base)]
+
+
+def test_permute_row_keeps_state_validity():
+    cfg = cfg_of(3)
+    for r in rtla.random_rows(cfg, 0, 30):
+        img = rtla.permute_row(cfg, r, [2, 0, 1])
+        assert rtla.row_fingerprint(cfg, img) == rtla.stored_fingerprint(img)
+        back = rtla.permute_row(cfg, img, [1, 2, 0])  # the inverse permutation
+        assert back == r
+    with pytest.raises(rtla.RtlaError):
+        rtla.permute_row(cfg, r, [0, 0, 1])
