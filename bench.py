@@ -394,7 +394,8 @@ def main():
             dist.destroy_process_group()
         else:
             cid = bytes(range(128))
-        print("bench.py rank %d of %d ready (id %s)" % (rank, world, cid[:4].hex()), flush=True)
+        sys.stdout.write("bench.py rank %d of %d ready (id %s)\n" % (rank, world, cid[:4].hex()))  # one write per line
+        sys.stdout.flush()
         return
     import rtla
     comm_id = None

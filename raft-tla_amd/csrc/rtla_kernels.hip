@@ -453,17 +453,17 @@ __host__ __device__ constexpr int lane_lds_words(int W, int AW) { return 64 * W 
 namespace {
 
 constexpr int RING = 128;   // pair ring (u16: state lane << 8 | instance - window base)
-constexpr int NEWCAP = 128; // new-state list (u64 parent records)
+constexpr int NEWCAP = 256; // new-state list (u16: state lane << 8 | instance)
 
 constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
 
 // Per-wave LDS of k_expand_compact (16-byte aligned pieces first):
 // per-state fingerprint with allLogs' applied (GROUP FPs) | SYMMETRY: the
 // fingerprint of each state's allLogs' (GROUP FPs) | per-owner (base, used)
-// of the open outbox chunk | pending new states (NEWCAP parent records) |
+// of the open outbox chunk | pending new states (NEWCAP u16 entries) |
 // GROUP rows | allLogs' words of each state | pair ring.
 __host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym) {
-  return (4 * GROUP * (sym ? 2 : 1) + 4 * SHARD_MAX + 2 * NEWCAP + GROUP * W + GROUP * AW + RING / 2 + 3) & ~3;
+  return (4 * GROUP * (sym ? 2 : 1) + 4 * SHARD_MAX + NEWCAP / 2 + GROUP * W + GROUP * AW + RING / 2 + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -593,7 +593,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   FP* afpl = pfpl + GROUP;               // SYM [state lane]: fingerprint of its allLogs'
   unsigned long long* obox =             // [o] base of the open chunk, [SHARD_MAX + o] used
       reinterpret_cast<unsigned long long*>(wl + 4 * GROUP * (SYM ? 2 : 1));
-  unsigned long long* newl = obox + 2 * SHARD_MAX;
+  uint16_t* newl = reinterpret_cast<uint16_t*>(obox + 2 * SHARD_MAX);
   uint32_t* rows = reinterpret_cast<uint32_t*>(newl + NEWCAP);
   uint32_t* pall = rows + GROUP * W;  // allLogs' words of state lane l: pall[l + w * GROUP]
   const StridedWords<GROUP> pall_mine{pall + (lane & (GROUP - 1))};
@@ -620,10 +620,24 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   unsigned long long pold = 0;
   FP pf{0, 0};       // its fingerprint (home slot and owner derive from it)
   uint32_t pinfo = 0;  // its state lane << 16 | action instance
+  // Single shard: a probe whose home-slot load did not show its key issues
+  // ONE CAS -- at the home slot if it read empty, else at the next slot
+  // (linear probing; slots only ever go 0 -> key) -- together with the next
+  // chunk's loads, and that CAS is resolved a chunk later: neither the
+  // insert nor the first collision step waits for a round trip.
+  const bool async_cas = !MULTI && !(xflags & XF_CAS_ONLY);
+  bool cpend = false;    // CAS set up by resolve(), issued by issue_cas()
+  bool cflight = false;  // CAS in flight (result in cold)
+  unsigned long long cold = 0, ckey = 0, cidx = 0;
+  uint32_t cinfo = 0;
   // New states found so far whose rows are not built yet: newl[head, tail)
-  // (mod NEWCAP) holds their parent records; their parents are rows of the
-  // current group (uniform counters).
+  // (mod NEWCAP) holds (state lane, instance); their parents are rows of the
+  // current group (uniform counters).  A reservation of next-level slots for
+  // the oldest 64 is requested one chunk before they are built (res_ob: the
+  // atomic's result in lane 0, read only then).
   int head = 0, tail = 0;
+  bool have_res = false;
+  unsigned long long res_ob = 0;
   unsigned long long dedup_new = 0;  // XF_DEDUP_ONLY: new fingerprints (uniform)
   unsigned long long s0 = 0;  // first state of the current group
 #ifdef RTLA_PFP_SHFL
@@ -632,13 +646,17 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 
   // One atomic reserves nb next-level slots.  Slots past next_cap are
   // dropped and flagged (the level is then reported incomplete).
-  auto reserve = [&](int nb) {
+  auto reserve_issue = [&](int nb) {  // the atomic, not waited for
     unsigned long long ob = 0;
     if (lane == 0) ob = atomicAdd(&ctr->next_count, (unsigned long long)nb);
+    return ob;
+  };
+  auto reserve_take = [&](unsigned long long ob, int nb) {
     ob = shfl0_u64(ob);
     if (ob + nb > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
     return ob;
   };
+  auto reserve = [&](int nb) { return reserve_take(reserve_issue(nb), nb); };
   // Build the rows of the nb oldest pending new states into slots obase ..
   // obase + nb - 1 of the next level, one state per lane:
   //  (1) the wave copies each parent row (LDS) to its child's slot with
@@ -653,9 +671,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // parent-row gather, no second launch.
   auto build_rows = [&](unsigned long long obase, int nb) {
     const bool act = lane < nb;
-    const unsigned long long pr = act ? newl[(head + lane) & (NEWCAP - 1)] : 0ull;
-    const int sl = act ? (int)(((pr >> 16) & ((1ull << 40) - 1ull)) - (cur_base + s0)) : 0;
-    const int inst = (int)(pr & 0xffffull);
+    const int e = act ? newl[(head + lane) & (NEWCAP - 1)] : 0;
+    const int sl = e >> 8, inst = e & 255;
     const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nb, next_cap - obase);
     const bool rows_on = !(xflags & XF_NO_MATERIALIZE) && RTLA_IDX_OK(ctr, obase + nrows, ctr->cap_next + 1);
     const unsigned long long p0 = ring_idx(next, obase);
@@ -722,15 +739,38 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       }
     }
     if (lane < nrows && RTLA_IDX_OK(ctr, next_base + obase + lane, ctr->cap_parents))
-      parents[next_base + obase + lane] = pr;
+      parents[next_base + obase + lane] =
+          (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
     head += nb;
+  };
+  auto issue_cas = [&]() {
+    if (cpend) cold = atomicCAS(&table[cidx], 0ull, ckey);
+    cflight = cpend;
+    cpend = false;
   };
   auto resolve = [&]() {
     bool isnew = false;
+    uint32_t ninfo = pinfo;  // the state isnew refers to
     const int powner = MULTI ? fp_owner(pf, box.nshard) : me;
     const unsigned long long prec =
         (unsigned long long)me << 56 | (cur_base + s0 + (pinfo >> 16)) << 16 | (unsigned long long)(pinfo & 0xffffu);
-    if (pend) {
+    if (async_cas) {
+      if (cflight) {  // the CAS issued one chunk ago
+        if (cold == 0ull) isnew = true;
+        else if (cold != ckey) isnew = fpset_resolve(table, tlog2, ckey, cidx, cold, ctr);  // rare: keep probing
+      }
+      ninfo = cinfo;
+      cflight = false;
+      if (pend) {  // this chunk's load -> seen, or a CAS for the next issue
+        const unsigned long long key = pf.b | 1ull, idx = pf.a >> (64 - tlog2);
+        if (pold != key) {
+          cidx = pold == 0ull ? idx : ((idx + 1ull) & ((1ull << tlog2) - 1ull));
+          ckey = key;
+          cinfo = pinfo;
+          cpend = true;
+        }
+      }
+    } else if (pend) {
       const bool to_sent = MULTI && powner != me;
       unsigned long long* t = to_sent ? sent : table;
       const unsigned long long pidx = pf.a >> (64 - tlog2);
@@ -777,7 +817,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     if (m && (xflags & XF_DEDUP_ONLY)) {  // synthetic microbench: count, keep no row
       dedup_new += __popcll(m);
     } else if (m) {
-      if (isnew) newl[(tail + __popcll(m & lanes_below)) & (NEWCAP - 1)] = prec;
+      if (isnew) newl[(tail + __popcll(m & lanes_below)) & (NEWCAP - 1)] = (uint16_t)((ninfo >> 16) << 8 | (ninfo & 255u));
       tail += __popcll(m);
       wave_sync();
     }
@@ -940,13 +980,21 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         STAMP(2);  // successor deltas, fingerprints, coverage, out-of-model invariants
         resolve();  // the previous chunk's probes, after this chunk's arithmetic
         STAMP(3);
-        // 64 new states pending: reserve their slots now (the returning
-        // atomic waits only for itself: every older load has been consumed),
-        // build their rows after this chunk's probes are issued
-        const bool flush = tail - head >= 64;
-        unsigned long long fbase = 0;
-        if (flush) fbase = reserve(64);
+        // Rows of the oldest 64 pending new states, into the slots reserved
+        // one chunk ago -- before this chunk's probes are issued, so the
+        // row stores' completion wait (build_rows step 3) never waits for
+        // them.  Then reserve for the next 64 if they are pending already.
+        if (have_res) {
+          build_rows(reserve_take(res_ob, 64), 64);
+          have_res = false;
+        }
+        STAMP(5);
+        if (tail - head >= 64) {
+          res_ob = reserve_issue(64);
+          have_res = true;
+        }
         asm volatile("" ::: "memory");
+        issue_cas();
         if (probe) {
           my_probe++;
           pend = true;
@@ -960,14 +1008,20 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
                                         : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         STAMP(4);  // slot reservation, probe issue
-        if (flush) build_rows(fbase, 64);
-        STAMP(5);
         done += cnt;
       }
     }
     // Group end: the last probes and every pending row (their parents are
     // this group's rows, which the next group overwrites).
     resolve();
+    if (async_cas) {  // the CAS this resolve set up, then its result
+      issue_cas();
+      resolve();
+    }
+    if (have_res) {
+      build_rows(reserve_take(res_ob, 64), 64);
+      have_res = false;
+    }
     while (tail > head) {
       const int nb = min(64, tail - head);
       build_rows(reserve(nb), nb);
@@ -1400,6 +1454,7 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
     done = true;                                                                                   \
   }
     bool done = false;
+#ifndef RTLA_EXP_MINIMAL  // perf experiments: compiled-in layouts only (fast builds)
     if (L.sym) {
 #define RTLA_SYMN(n) \
   case n: e = launch_compact<n, 32, Layout{}, true>(RTLA_ARGS); break;
@@ -1413,12 +1468,16 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
 #undef RTLA_SYMN
       done = true;
     }
+#endif
     if (!done && !(xflags & XF_NO_SPECIAL)) {
       RTLA_SPEC(CFG2)
       RTLA_SPEC(CFG1)
       RTLA_SPEC(EXHAUST)
     }
     if (!done) {  // run-time layout
+#ifdef RTLA_EXP_MINIMAL
+      return hipErrorNotSupported;
+#else
       const bool g64 = compact_group(L) == 64;
 #define RTLA_GENERIC(n) \
   case n: e = g64 ? launch_compact<n, 64, Layout{}>(RTLA_ARGS) : launch_compact<n, 32, Layout{}>(RTLA_ARGS); break;
@@ -1430,6 +1489,7 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
         default: RTLA_GENERIC(5)
       }
 #undef RTLA_GENERIC
+#endif
     }
 #undef RTLA_SPEC
 #undef RTLA_ARGS

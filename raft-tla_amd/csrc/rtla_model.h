@@ -295,7 +295,42 @@ RTLA_HD FP hash_words(uint64_t tag, P w, int n) {
   return FP{a, b};
 }
 enum { TAG_SRV = 1, TAG_MSG = 2, TAG_ALL = 3, TAG_ELEC = 4 };
-RTLA_HD FP h_srv(int i, const uint32_t* rec, int SW) { return hash_words((uint64_t)(TAG_SRV << 8 | i), rec, SW); }
+// First hash state of a record hashed at position p (run-time p < NS):
+// hash_words' tag mixing of TAG_SRV << 8 | p, folded to constants.
+template <int NS>
+RTLA_HD FP srv_seed(int p) {
+  FP s{0, 0};
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    const uint64_t tag = (uint64_t)(TAG_SRV << 8 | k);
+    if (k == p) {
+      s.a = mix_a(tag * 0x9E3779B97F4A7C15ull + 0x243f6a8885a308d3ull);
+      s.b = mix_b(tag * 0xD1B54A32D192ED03ull + 0x13198a2e03707344ull);
+    }
+  }
+  return s;
+}
+template <int N>
+RTLA_HD FP hash_words_from(FP s, const uint32_t* w) {  // = hash_words(tag, w, N) given its seed s
+#pragma unroll
+  for (int k = 0; k < N; k += 2) {
+    const uint64_t x = (uint64_t)w[k] | ((k + 1 < N) ? (uint64_t)w[k + 1] << 32 : 0ull);
+    s.a = mix_a(s.a ^ x);
+    s.b = mix_b(s.b + x);
+  }
+  return s;
+}
+
+// = hash_words(TAG_SRV << 8 | i, rec, SW), the tag's mixing folded to constants
+RTLA_HD FP h_srv(int i, const uint32_t* rec, int SW) {
+  FP s = srv_seed<NMAX>(i);
+  for (int k = 0; k < SW; k += 2) {
+    const uint64_t x = (uint64_t)rec[k] | ((k + 1 < SW) ? (uint64_t)rec[k + 1] << 32 : 0ull);
+    s.a = mix_a(s.a ^ x);
+    s.b = mix_b(s.b + x);
+  }
+  return s;
+}
 RTLA_HD FP h_msg(uint64_t slot) { return slot ? hash_u64(TAG_MSG, slot) : FP{0, 0}; }
 RTLA_HD FP h_all(int idx) { return hash_u64(TAG_ALL, (uint64_t)idx); }
 RTLA_HD FP h_elec(const uint32_t* rec, int EW) { return hash_words(TAG_ELEC, rec, EW); }
@@ -1021,32 +1056,6 @@ RTLA_HD uint32_t srv_sig(int i, const uint32_t* rec) {
     else others += x;
   }
   return mix32(h ^ mix32(others + 0x85ebca6bu));
-}
-
-// First hash state of a record hashed at position p (run-time p < NS):
-// hash_words' tag mixing of TAG_SRV << 8 | p, folded to constants.
-template <int NS>
-RTLA_HD FP srv_seed(int p) {
-  FP s{0, 0};
-#pragma unroll
-  for (int k = 0; k < NS; k++) {
-    const uint64_t tag = (uint64_t)(TAG_SRV << 8 | k);
-    if (k == p) {
-      s.a = mix_a(tag * 0x9E3779B97F4A7C15ull + 0x243f6a8885a308d3ull);
-      s.b = mix_b(tag * 0xD1B54A32D192ED03ull + 0x13198a2e03707344ull);
-    }
-  }
-  return s;
-}
-template <int N>
-RTLA_HD FP hash_words_from(FP s, const uint32_t* w) {  // = hash_words(tag, w, N) given its seed s
-#pragma unroll
-  for (int k = 0; k < N; k += 2) {
-    const uint64_t x = (uint64_t)w[k] | ((k + 1 < N) ? (uint64_t)w[k + 1] << 32 : 0ull);
-    s.a = mix_a(s.a ^ x);
-    s.b = mix_b(s.b + x);
-  }
-  return s;
 }
 
 RTLA_HD bool fp_less(FP x, FP y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }

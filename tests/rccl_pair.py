@@ -1,0 +1,47 @@
+"""One rank of a world-size-N BFS over RCCL (test helper, run as a child
+process by test_gpu.py::test_rccl_ranks_match_golden): rank 0 writes the
+RCCL unique id to a file, the other ranks poll for it -- the CLI's
+rendezvous -- then every rank runs the golden model and rank 0 prints the
+per-level counts as JSON.  Ranks share the device when the box has fewer
+GPUs than ranks (device = rank % device count)."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "raft-tla_amd"))
+import rtla  # noqa: E402
+
+
+def main():
+    rank, world, idfile, name = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bfs_counts.json")))[name]
+    if rank == 0:
+        cid = rtla.comm_id()
+        with open(idfile + ".tmp", "wb") as f:
+            f.write(cid)
+        os.rename(idfile + ".tmp", idfile)
+    else:
+        t0 = time.time()
+        while not os.path.exists(idfile):
+            if time.time() - t0 > 60:
+                raise SystemExit("rank %d: no RCCL id after 60 s" % rank)
+            time.sleep(0.05)
+        cid = open(idfile, "rb").read()
+    log2 = max(16, (int(g["distinct"] * 2)).bit_length())
+    cfg = rtla.Config(g["n_server"], g["n_value"], g["max_term"], g["max_log"], g["max_copies"], g["max_msgs"],
+                      tuple(g["invariants"]), fpset_log2=log2, mem_budget=(8 << log2) * 3 + (1 << 29),
+                      symmetry=bool(g.get("symmetry", False)), chunk=int(os.environ.get("RCCL_PAIR_CHUNK", "0")))
+    levels = []
+    with rtla.Checker(cfg, rank=rank, world=world, comm_id=cid) as ck:
+        st = ck.init()
+        while st == rtla.OK:
+            st = ck.step()
+        levels = [[lv.new, lv.generated] for lv in ck.levels]
+        out = {"rank": rank, "levels": levels, "distinct": ck.distinct, "generated": ck.generated,
+               "status": st, "info": ck.device_info() if hasattr(ck, "device_info") else ""}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

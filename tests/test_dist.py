@@ -4,6 +4,7 @@ time as the max over ranks.  The device data path
 (RCCL all-to-all-v between shards) is covered on one GPU by the virtual-shard
 tests in test_gpu.py."""
 import os
+import re
 import socket
 import sys
 
@@ -77,7 +78,7 @@ def test_bench_gpus_flag_launches_ranks():
                          capture_output=True, text=True, timeout=240,
                          env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert out.returncode == 0, out.stdout + out.stderr
-    lines = sorted(l for l in out.stdout.splitlines() if l.startswith("bench.py rank"))
+    lines = sorted(re.findall(r"bench\.py rank \d of \d ready \(id [0-9a-f]+\)", out.stdout))
     assert lines == ["bench.py rank 0 of 2 ready (id 00010203)", "bench.py rank 1 of 2 ready (id 00010203)"], \
         out.stdout + out.stderr
 
