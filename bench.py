@@ -90,12 +90,13 @@ LOAD_PER_S = 4.66e10
 
 
 def load_traffic(workload):
-    """HBM bytes of the probe kernel per launch from the committed PMC profile
-    (profiles/*/traffic.json, written by tools/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this workload), or None."""
+    """HBM bytes of the level kernel per launch from the newest committed PMC
+    profile of this workload (profiles/<round>/traffic*.json, written by
+    tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3
+    passes), or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic*.json"))):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):

@@ -77,13 +77,30 @@ for wdir in sorted(glob.glob(os.path.join(root, "*", "kt"))):
     if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
         fetch = agg["FETCH_SIZE"] * 1024 / nd["p1"]
         write = agg["WRITE_SIZE"] * 1024 / nd["p2"]
+        # probes per launch from the bench line of the kernel-trace run
+        probes = None
+        try:
+            kt_log = open(os.path.join(root, "%s.kt.log" % w)).read()
+            b = json.loads([l for l in kt_log.splitlines() if l.startswith('{"metric"')][-1])
+            ra = b["roofline"]["random_access"]
+            probes = ra["probes_per_s"] * b["roofline"]["kernel_ms_avg"] / 1e3
+        except (OSError, ValueError, KeyError, IndexError):
+            pass
+        per_load = calib["FETCH_SIZE"]["probe_seen_load_bytes_per_access"]
+        if probes is not None:  # random probe loads count ~64 B each; the rest is the row streams
+            probe_fetch = probes * per_load
+            fetch_true = probe_fetch + max(0.0, fetch - probe_fetch) / stream_f
+        else:
+            fetch_true = fetch / stream_f
         t = {"workload": w, "kernel": "k_expand_compact", "launches": nd["p1"],
              "fetch_bytes_per_launch_raw": fetch, "write_bytes_per_launch_raw": write,
-             "fetch_bytes_per_launch": fetch / stream_f, "write_bytes_per_launch": write,
+             "probes_per_launch": probes,
+             "fetch_bytes_per_launch": fetch_true, "write_bytes_per_launch": write,
              "calibration": calib,
-             "note": "FETCH_SIZE divided by the counted/true ratio of a known row stream "
-                     "(tools/fetch_calib.py: the level kernel reading E rows and nothing else); WRITE_SIZE as "
-                     "counted. Random 8-B fingerprint-set accesses count as the calibration's bytes per access."}
+             "note": "FETCH_SIZE: the fingerprint-set probe loads (probes per launch from the bench line x the "
+                     "calibrated counted bytes per random load, ~64 B) plus the remainder divided by the "
+                     "counted/true ratio of a known row stream (tools/fetch_calib.py: the level kernel reading E "
+                     "rows and nothing else).  WRITE_SIZE as counted (each fingerprint-set CAS counts ~68 B)."}
         t["bytes_per_launch"] = t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"]
         json.dump(t, open(os.path.join(dest, "traffic_%s.json" % w), "w"), indent=1)
         lines.append("   HBM bytes per launch: fetch %.4g (raw %.4g) + write %.4g = %.4g" % (
