@@ -553,7 +553,10 @@ int main(int argc, char** argv) {
     printf("  Estimates of the probability that TLC did not check all reachable states\n"
            "  because two distinct states had the same fingerprint:\n"
            "  calculated (optimistic):  val = %.1E\n",
-           (double)ls.distinct_total * (double)ls.generated_total / 3.4028236692093846e38);
+           // The set stores 63 bits of the fingerprint (fp.b | 1) at a slot
+           // chosen by fp.a; a probe walks ~2 slots at the loads used, so
+           // each generated state is compared with ~2 random 63-bit keys.
+           (double)ls.generated_total * 2.0 / 9.223372036854775808e18);
   }
   if (coverage) {
     uint64_t g[16], d[16];

@@ -462,8 +462,11 @@ constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a 
 // fingerprint of each state's allLogs' (GROUP FPs) | per-owner (base, used)
 // of the open outbox chunk | pending new states (NEWCAP u16 entries) |
 // GROUP rows | allLogs' words of each state | pair ring.
-__host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym) {
-  return (4 * GROUP * (sym ? 2 : 1) + 4 * SHARD_MAX + NEWCAP / 2 + GROUP * W + GROUP * AW + RING / 2 + 3) & ~3;
+// (The outbox state exists only in the MULTI kernels: one shard's tile then
+// stays small enough for 12 one-wave blocks per CU on configs[1]'s 372-byte rows.)
+__host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym, bool multi) {
+  return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW + RING / 2 +
+          3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -588,12 +591,12 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   __shared__ unsigned int cov[2 * COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = L.W, AW = L.all_words;
-  uint32_t* wl = lds + wave * compact_lds_words(W, AW, GROUP, SYM);
+  uint32_t* wl = lds + wave * compact_lds_words(W, AW, GROUP, SYM, MULTI);
   FP* pfpl = reinterpret_cast<FP*>(wl);  // [state lane]: its fingerprint + the allLogs' change (raft.tla:465)
   FP* afpl = pfpl + GROUP;               // SYM [state lane]: fingerprint of its allLogs'
   unsigned long long* obox =             // [o] base of the open chunk, [SHARD_MAX + o] used
       reinterpret_cast<unsigned long long*>(wl + 4 * GROUP * (SYM ? 2 : 1));
-  uint16_t* newl = reinterpret_cast<uint16_t*>(obox + 2 * SHARD_MAX);
+  uint16_t* newl = reinterpret_cast<uint16_t*>(obox + (MULTI ? 2 * SHARD_MAX : 0));
   uint32_t* rows = reinterpret_cast<uint32_t*>(newl + NEWCAP);
   uint32_t* pall = rows + GROUP * W;  // allLogs' words of state lane l: pall[l + w * GROUP]
   const StridedWords<GROUP> pall_mine{pall + (lane & (GROUP - 1))};
@@ -656,7 +659,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     if (ob + nb > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
     return ob;
   };
-  auto reserve = [&](int nb) { return reserve_take(reserve_issue(nb), nb); };
   // Build the rows of the nb oldest pending new states into slots obase ..
   // obase + nb - 1 of the next level, one state per lane:
   //  (1) the wave copies each parent row (LDS) to its child's slot with
@@ -1024,7 +1026,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     }
     while (tail > head) {
       const int nb = min(64, tail - head);
-      build_rows(reserve(nb), nb);
+      build_rows(reserve_take(reserve_issue(nb), nb), nb);
     }
     wave_sync();
     STAMP(6);  // group-end drain
@@ -1360,7 +1362,7 @@ int expand_lane_wpb(const Layout& L) {
 // not the tile, bounds that kernel).
 constexpr int compact_group(const Layout& L) {
   if (L.sym) return 32;
-  return compact_lds_words(L.W, L.all_words, 64, false) * sizeof(uint32_t) <= RTLA_GROUP64_LDS ? 64 : 32;
+  return compact_lds_words(L.W, L.all_words, 64, false, true) * sizeof(uint32_t) <= RTLA_GROUP64_LDS ? 64 : 32;
 }
 
 static int device_cus() {
@@ -1376,7 +1378,7 @@ static int device_cus() {
 
 
 int expand_compact_wpb(const Layout& L) {
-  const size_t per = (size_t)compact_lds_words(L.W, L.all_words, compact_group(L), L.sym) * sizeof(uint32_t);
+  const size_t per = (size_t)compact_lds_words(L.W, L.all_words, compact_group(L), L.sym, true) * sizeof(uint32_t);
   // one wave may use up to the CU's 160 KiB of LDS; instance ids fit 8 bits per 64-instance window
   if (per > 160 * 1024 || ((L.fam[F_COUNT] + 63) / 64) * 64 > 256) return 0;
   return per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
@@ -1415,13 +1417,15 @@ static hipError_t launch_compact(const Layout& L, bool multi, const Ring& cur, u
   auto kfn = multi ? k_expand_compact<NS, true, GROUP, LC, SYM> : k_expand_compact<NS, false, GROUP, LC, SYM>;
   const uint64_t groups = (s_end - s_begin + GROUP - 1) / GROUP;
   uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
-  const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words, GROUP, SYM) * sizeof(uint32_t);
+  const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words, GROUP, SYM, multi) * sizeof(uint32_t);
   if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
     static int per_cu[2][2];  // per instantiation: [multi][one-wave blocks]
     int& pc = per_cu[multi][wpb == 1];
     if (!pc) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kfn, 64 * wpb, lds) != hipSuccess || pc < 1)
         pc = 16 / wpb;
+      if (const char* e = getenv("RTLA_BLOCKS_PER_CU"))  // occupancy experiments
+        if (atoi(e) > 0) pc = std::min(pc, atoi(e));
     }
     blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * pc);
   }
