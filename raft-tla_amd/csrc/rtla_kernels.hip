@@ -1364,6 +1364,17 @@ constexpr int compact_group(const Layout& L) {
   if (L.sym) return 32;
   return compact_lds_words(L.W, L.all_words, 64, false, true) * sizeof(uint32_t) <= RTLA_GROUP64_LDS ? 64 : 32;
 }
+// The compiled-in configurations may also run 16-state groups: wide rows
+// (configs[2]: 516 B, configs[3]: 628 B) would otherwise leave the 32-row
+// tile, not the registers, bounding the waves per CU (8 and 7 instead of
+// 12 and 8; bench's occupancy sweep: throughput grows with resident waves).
+#ifndef RTLA_GROUP32_LDS
+#define RTLA_GROUP32_LDS (19 * 1024)
+#endif
+constexpr int spec_group(const Layout& L) {
+  const int g = compact_group(L);
+  return g == 32 && compact_lds_words(L.W, L.all_words, 32, L.sym, true) * sizeof(uint32_t) > RTLA_GROUP32_LDS ? 16 : g;
+}
 
 static int device_cus() {
   static int cus = 0;
@@ -1406,7 +1417,15 @@ namespace specs {
 constexpr Layout CFG2 = layout_of(3, 2, 3, 2, 1, 0, 18, 6, INV_ELECTION_SAFETY | INV_LOG_MATCHING);  // configs[1]
 constexpr Layout CFG1 = layout_of(3, 1, 2, 1, 1, 0, 24, 3, INV_NO_TWO_LEADERS);                     // configs[0]
 constexpr Layout EXHAUST = layout_of(3, 2, 2, 2, 1, 2, 3, 3, INV_ELECTION_SAFETY | INV_LOG_MATCHING);
-static_assert(CFG2.N == 3 && CFG1.N == 3 && EXHAUST.N == 3, "compiled-in layouts must be valid");
+constexpr Layout CFG3 = layout_of(3, 2, 4, 3, 2, 0, 20, 9, 0);                                      // configs[2]
+constexpr Layout SYNTH = layout_of(3, 2, 4, 3, 2, 0, 12, 9, INV_ELECTION_SAFETY | INV_LOG_MATCHING);  // configs[4]
+constexpr Layout symmetric(Layout l) {
+  l.sym = 1;
+  return l;
+}
+constexpr Layout CFG4 = symmetric(layout_of(5, 1, 3, 2, 1, 0, 20, 10, 0));  // configs[3], SYMMETRY
+static_assert(CFG2.N == 3 && CFG1.N == 3 && EXHAUST.N == 3 && CFG3.N == 3 && SYNTH.N == 3 && CFG4.N == 5,
+              "compiled-in layouts must be valid");
 }  // namespace specs
 
 template <int NS, int GROUP, Layout LC, bool SYM = false>
@@ -1454,12 +1473,13 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
                   st, xflags, sent, wpb
 #define RTLA_SPEC(S)                                                                               \
   if (!done && same_layout(L, specs::S)) {                                                         \
-    e = launch_compact<specs::S.N, compact_group(specs::S), specs::S>(RTLA_ARGS);                  \
+    e = launch_compact<specs::S.N, spec_group(specs::S), specs::S, (bool)specs::S.sym>(RTLA_ARGS);   \
     done = true;                                                                                   \
   }
     bool done = false;
+    if (L.sym && !(xflags & XF_NO_SPECIAL)) RTLA_SPEC(CFG4)
 #ifndef RTLA_EXP_MINIMAL  // perf experiments: compiled-in layouts only (fast builds)
-    if (L.sym) {
+    if (!done && L.sym) {
 #define RTLA_SYMN(n) \
   case n: e = launch_compact<n, 32, Layout{}, true>(RTLA_ARGS); break;
       switch (L.N) {
@@ -1477,6 +1497,8 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
       RTLA_SPEC(CFG2)
       RTLA_SPEC(CFG1)
       RTLA_SPEC(EXHAUST)
+      RTLA_SPEC(CFG3)
+      RTLA_SPEC(SYNTH)
     }
     if (!done) {  // run-time layout
 #ifdef RTLA_EXP_MINIMAL

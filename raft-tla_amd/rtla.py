@@ -97,6 +97,8 @@ def _load():
         "rtla_probe_bench": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_uint64)]),
         "rtla_random_rows": (C.c_int, [P(_Cfg), C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, P(C.c_uint32)]),
         "rtla_synthetic_step": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, P(_Stats)]),
+        "rtla_synthetic_generate": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]),
+        "rtla_synthetic_dedup": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(_Stats)]),
         "rtla_orbit_key": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_uint64), P(C.c_int)]),
         "rtla_permute_row": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_int), P(C.c_uint32)]),
     }
@@ -114,7 +116,7 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
             "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step",
-            "rtla_orbit_key", "rtla_permute_row"]
+            "rtla_synthetic_generate", "rtla_synthetic_dedup", "rtla_orbit_key", "rtla_permute_row"]
 
 SYNTH_SEED = 0x5AF72025  # the synthetic microbench's PRNG seed
 
@@ -418,6 +420,19 @@ class Checker:
         rc = _lib.rtla_synthetic_step(self._h, seed, first, n, pool, C.byref(st))
         if rc < 0:
             raise RtlaError(rc, "rtla_synthetic_step", st.flags)
+        return Level(0, st.frontier, st.new_states, st.generated, st.seconds, st.kernel_ms, st.probes, st.row_bytes,
+                     st.expand_ms)
+
+    def synthetic_generate(self, first: int, n: int, pool: int = 0, at: int = 0, seed: int = SYNTH_SEED):
+        """Input states first .. first + n - 1 into row-arena rows at .. at + n - 1 (on the device)."""
+        _check(_lib.rtla_synthetic_generate(self._h, seed, first, n, pool, at), "rtla_synthetic_generate")
+
+    def synthetic_dedup(self, begin: int, end: int) -> Level:
+        """One dedup-only level-kernel launch over the resident arena rows [begin, end)."""
+        st = _Stats()
+        rc = _lib.rtla_synthetic_dedup(self._h, begin, end, C.byref(st))
+        if rc < 0:
+            raise RtlaError(rc, "rtla_synthetic_dedup", st.flags)
         return Level(0, st.frontier, st.new_states, st.generated, st.seconds, st.kernel_ms, st.probes, st.row_bytes,
                      st.expand_ms)
 

@@ -52,6 +52,8 @@ PREFIXES = {
     # BASELINE.json configs[1] and configs[0] exactly as stated (no in-flight bound)
     "n3_v2_t3_l2_c1_prefix": (3, 2, 3, 2, 1, 0, (ES, LM), 25_000_000),
     "n3_v1_t2_l1_c1_prefix": (3, 1, 2, 1, 1, 0, (NTL,), 30_000_000),
+    # BASELINE.json configs[2] as stated (2 copies per message: Duplicate/Drop live)
+    "n3_v2_t4_l3_c2_prefix": (3, 2, 4, 3, 2, 0, (), 20_000_000),
 }
 # SYMMETRY prefixes (orbit counts per level; no text hashes: the orbit
 # representatives kept differ between implementations).  N = 4 and BASELINE

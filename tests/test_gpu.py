@@ -187,7 +187,8 @@ def test_full_size_counts_match_golden(name):
 
 # bench.py's row formats (bag slots) for the prefix models: the same layouts
 # the bench runs, i.e. the kernels compiled for them (rtla_kernels.hip specs)
-PREFIX_BAG = {"n3_v2_t3_l2_c1_prefix": 18, "n3_v1_t2_l1_c1_prefix": 24, "n5_v1_t3_l2_c1_sym_prefix": 20}
+PREFIX_BAG = {"n3_v2_t3_l2_c1_prefix": 18, "n3_v1_t2_l1_c1_prefix": 24, "n5_v1_t3_l2_c1_sym_prefix": 20,
+              "n3_v2_t4_l3_c2_prefix": 20}
 
 
 def level_text_hash(cfg, rows):
@@ -614,3 +615,22 @@ def test_synthetic_step_dedup_counts():
     with rtla.Checker(cfg) as ck:
         got = [ck.synthetic_step(b * n, n, pool) for b in range(2)]
     assert [(lv.generated, lv.probes, lv.new) for lv in got] == expect
+
+
+def test_synthetic_resident_dedup_matches_step():
+    """bench.py's configs[4] path: inputs generated into the row arena once
+    (rtla_synthetic_generate), then dedup passes over resident row ranges
+    (rtla_synthetic_dedup) -- the same counts as generate-and-dedup steps."""
+    cfg = rtla.Config(**SYNTH, fpset_log2=22, mem_budget=1 << 30)
+    n, pool = 2560, 400  # range starts are multiples of 64 (level-kernel groups)
+    with rtla.Checker(cfg) as ck:
+        want = [ck.synthetic_step(b * n, n, pool) for b in range(2)]
+        ck.reset()
+        ck.synthetic_generate(n, n, pool, at=n)  # out of order: rows land where `at` says
+        ck.synthetic_generate(0, n, pool, at=0)
+        got = [ck.synthetic_dedup(0, n), ck.synthetic_dedup(n, 2 * n)]
+    assert [(lv.frontier, lv.generated, lv.probes, lv.new) for lv in got] == \
+        [(lv.frontier, lv.generated, lv.probes, lv.new) for lv in want]
+    with pytest.raises(rtla.RtlaError):
+        with rtla.Checker(cfg) as ck:
+            ck.synthetic_dedup(10, n)  # not a group boundary
