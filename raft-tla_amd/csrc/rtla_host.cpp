@@ -35,12 +35,16 @@
 //      parent's shard, so traces walk across shards.
 // Then one all-reduce of {new, generated, probes, violation, flags} decides
 // termination (TLC's "0 states left on queue").
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sched.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <string>
@@ -93,6 +97,23 @@ struct Shard {
 
 }  // namespace
 
+// Host shared-memory transport for world > 1 (RTLA_TRANSPORT=shm): the same
+// collectives as the RCCL path, staged through a POSIX shared-memory segment
+// named after the communicator id.  It lets N processes on ONE GPU run the
+// multi-rank protocol -- RCCL refuses two ranks on one device -- so the
+// world > 1 control flow (count gathers, all-to-all-v, answer routing,
+// reductions, trace broadcasts, recovery checks) is tested on single-GPU
+// boxes.  Not a performance path: every operation synchronises the stream.
+struct ShmComm {
+  struct Header {
+    std::atomic<uint32_t> arrive, gen;
+  };
+  Header* hdr = nullptr;
+  uint8_t* data = nullptr;   // world x world slots of `slot` bytes: [src][dst]
+  size_t slot = 0, size = 0;
+  uint8_t* slot_at(int src, int dst, int world) const { return data + ((size_t)src * world + dst) * slot; }
+};
+
 struct rtla_ctx {
   rtla_cfg cfg;
   Layout L;
@@ -102,6 +123,7 @@ struct rtla_ctx {
   std::vector<Shard> sh;   // shards held by this process
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
+  ShmComm* shm = nullptr;  // RTLA_TRANSPORT=shm instead of RCCL
   int tlog2 = 0;
   uint64_t front_cap = 0, box_cap = 0, chunk = 0, rows_cap = 0;
   uint64_t* red = nullptr;  // device scratch for all-reduces
@@ -157,6 +179,151 @@ static hipError_t ring_copy(const Ring& r, int W, uint64_t g, uint64_t n, uint32
       return RTLA_E_COMM;                                                                             \
     }                                                                                                 \
   } while (0)
+
+// ---- collectives between ranks: RCCL, or the shared-memory transport (ShmComm)
+// Every function is called by every rank in the same order; device buffers,
+// in stream order.
+
+static int shm_barrier(rtla_ctx* x) {
+  ShmComm::Header* h = x->shm->hdr;
+  const uint32_t g = h->gen.load(std::memory_order_acquire);
+  if (h->arrive.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)x->world - 1) {
+    h->arrive.store(0, std::memory_order_relaxed);
+    h->gen.fetch_add(1, std::memory_order_acq_rel);
+    return RTLA_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  while (h->gen.load(std::memory_order_acquire) == g) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) {
+      fprintf(stderr, "rtla: shm transport: the other ranks did not arrive\n");
+      return RTLA_E_COMM;
+    }
+    sched_yield();
+  }
+  return RTLA_OK;
+}
+
+static int shm_open_comm(rtla_ctx* x, const void* comm_id) {
+  const uint8_t* id = static_cast<const uint8_t*>(comm_id);
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the 128-byte id
+  for (int i = 0; i < 128; i++) h = (h ^ id[i]) * 1099511628211ull;
+  char name[64];
+  snprintf(name, sizeof name, "/rtla_%016llx", (unsigned long long)h);
+  const char* e = getenv("RTLA_SHM_SLOT_MB");
+  const size_t slot = (size_t)(e && atoi(e) > 0 ? atoi(e) : 64) << 20;
+  const size_t size = 4096 + (size_t)x->world * x->world * slot;
+  const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+  if (fd < 0) return RTLA_E_COMM;
+  if (ftruncate(fd, (off_t)size) != 0) {
+    close(fd);
+    return RTLA_E_COMM;
+  }
+  void* p = mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return RTLA_E_COMM;
+  x->shm = new ShmComm();
+  x->shm->hdr = static_cast<ShmComm::Header*>(p);
+  x->shm->data = static_cast<uint8_t*>(p) + 4096;
+  x->shm->slot = slot;
+  x->shm->size = size;
+  const int rc = shm_barrier(x);  // every rank has the segment mapped: the name can go
+  if (x->rank == 0) shm_unlink(name);
+  return rc;
+}
+
+static int shm_too_big(size_t bytes, const ShmComm& c) {
+  if (bytes <= c.slot) return RTLA_OK;
+  fprintf(stderr, "rtla: shm transport: %zu-byte message exceeds the %zu-byte slot (RTLA_SHM_SLOT_MB)\n", bytes, c.slot);
+  return RTLA_E_COMM;
+}
+
+// In place: sum (op 0) or max (op 1) of n u64 over all ranks.
+static int comm_allreduce(rtla_ctx* x, uint64_t* buf, int n, int op) {
+  if (!x->shm) {
+    NCCLCHK(ncclAllReduce(buf, buf, n, ncclUint64, op ? ncclMax : ncclSum, x->comm, x->stream));
+    return RTLA_OK;
+  }
+  const ShmComm& c = *x->shm;
+  if (int rc = shm_too_big(8 * (size_t)n, c)) return rc;
+  HIPCHK(hipMemcpyAsync(c.slot_at(x->rank, 0, x->world), buf, 8 * n, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  if (int rc = shm_barrier(x)) return rc;
+  std::vector<uint64_t> acc(n, 0);
+  for (int r = 0; r < x->world; r++) {
+    const uint64_t* v = reinterpret_cast<const uint64_t*>(c.slot_at(r, 0, x->world));
+    for (int i = 0; i < n; i++) acc[i] = op ? std::max(acc[i], v[i]) : acc[i] + v[i];
+  }
+  if (int rc = shm_barrier(x)) return rc;
+  HIPCHK(hipMemcpyAsync(buf, acc.data(), 8 * n, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return RTLA_OK;
+}
+
+// recv[r * n + i] = send[i] of rank r.
+static int comm_allgather(rtla_ctx* x, const uint64_t* send, uint64_t* recv, int n) {
+  if (!x->shm) {
+    NCCLCHK(ncclAllGather(send, recv, n, ncclUint64, x->comm, x->stream));
+    return RTLA_OK;
+  }
+  const ShmComm& c = *x->shm;
+  if (int rc = shm_too_big(8 * (size_t)n, c)) return rc;
+  HIPCHK(hipMemcpyAsync(c.slot_at(x->rank, 0, x->world), send, 8 * n, hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  if (int rc = shm_barrier(x)) return rc;
+  for (int r = 0; r < x->world; r++)
+    HIPCHK(hipMemcpyAsync(recv + (size_t)r * n, c.slot_at(r, 0, x->world), 8 * n, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return shm_barrier(x);
+}
+
+static int comm_bcast(rtla_ctx* x, uint64_t* buf, int n, int root) {
+  if (!x->shm) {
+    NCCLCHK(ncclBroadcast(buf, buf, n, ncclUint64, root, x->comm, x->stream));
+    return RTLA_OK;
+  }
+  const ShmComm& c = *x->shm;
+  if (int rc = shm_too_big(8 * (size_t)n, c)) return rc;
+  if (x->rank == root) {
+    HIPCHK(hipMemcpyAsync(c.slot_at(root, 0, x->world), buf, 8 * n, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+  }
+  if (int rc = shm_barrier(x)) return rc;
+  if (x->rank != root) {
+    HIPCHK(hipMemcpyAsync(buf, c.slot_at(root, 0, x->world), 8 * n, hipMemcpyHostToDevice, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+  }
+  return shm_barrier(x);
+}
+
+// One all-to-all-v round: point-to-point messages (at most one send and one
+// receive per peer), all in flight together (one RCCL group).
+struct Msg {
+  void* ptr;
+  size_t bytes;
+  int peer;
+};
+static int comm_exchange(rtla_ctx* x, const std::vector<Msg>& sends, const std::vector<Msg>& recvs) {
+  if (!x->shm) {
+    NCCLCHK(ncclGroupStart());
+    for (const Msg& m : sends) NCCLCHK(ncclSend(m.ptr, m.bytes, ncclUint8, m.peer, x->comm, x->stream));
+    for (const Msg& m : recvs) NCCLCHK(ncclRecv(m.ptr, m.bytes, ncclUint8, m.peer, x->comm, x->stream));
+    NCCLCHK(ncclGroupEnd());
+    return RTLA_OK;
+  }
+  const ShmComm& c = *x->shm;
+  for (const Msg& m : sends) {
+    if (int rc = shm_too_big(m.bytes, c)) return rc;
+    HIPCHK(hipMemcpyAsync(c.slot_at(x->rank, m.peer, x->world), m.ptr, m.bytes, hipMemcpyDeviceToHost, x->stream));
+  }
+  HIPCHK(hipStreamSynchronize(x->stream));
+  if (int rc = shm_barrier(x)) return rc;
+  for (const Msg& m : recvs) {
+    if (int rc = shm_too_big(m.bytes, c)) return rc;
+    HIPCHK(hipMemcpyAsync(m.ptr, c.slot_at(m.peer, x->rank, x->world), m.bytes, hipMemcpyHostToDevice, x->stream));
+  }
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return shm_barrier(x);
+}
 
 static int layout_from_cfg(const rtla_cfg* c, Layout* L) {
   if (!c) return RTLA_E_ARG;
@@ -367,6 +534,14 @@ extern "C" int rtla_random_rows(const rtla_cfg* c, uint64_t seed, uint64_t first
 
 extern "C" int rtla_comm_id(void* out128) {
   if (!out128) return RTLA_E_ARG;
+  const char* tr = getenv("RTLA_TRANSPORT");
+  if (tr && !strcmp(tr, "shm")) {  // the id only names the shared-memory segment
+    uint64_t v[16];
+    const uint64_t t = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    for (int i = 0; i < 16; i++) v[i] = t * 0x9E3779B97F4A7C15ull + (uint64_t)getpid() * 0xBF58476D1CE4E5B9ull + i;
+    memcpy(out128, v, 128);
+    return RTLA_OK;
+  }
   ncclUniqueId id;
   NCCLCHK(ncclGetUniqueId(&id));
   static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
@@ -392,6 +567,10 @@ extern "C" void rtla_close(rtla_ctx* x) {
   for (auto& s : x->sh) free_shard(s);
   if (x->red) (void)hipFree(x->red);
   if (x->comm) ncclCommDestroy(x->comm);
+  if (x->shm) {
+    munmap(x->shm->hdr, x->shm->size);
+    delete x->shm;
+  }
   if (x->stream) (void)hipStreamDestroy(x->stream);
   delete x;
 }
@@ -469,9 +648,14 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   if (hipSetDevice(x->device) != hipSuccess) { delete x; return RTLA_E_HIP; }
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) { delete x; return RTLA_E_HIP; }
   if (world > 1) {
-    ncclUniqueId id;
-    memcpy(&id, comm_id, sizeof id);
-    if (ncclCommInitRank(&x->comm, world, id, rank) != ncclSuccess) { rtla_close(x); return RTLA_E_COMM; }
+    const char* tr = getenv("RTLA_TRANSPORT");
+    if (tr && !strcmp(tr, "shm")) {
+      if (shm_open_comm(x, comm_id) != RTLA_OK) { rtla_close(x); return RTLA_E_COMM; }
+    } else {
+      ncclUniqueId id;
+      memcpy(&id, comm_id, sizeof id);
+      if (ncclCommInitRank(&x->comm, world, id, rank) != ncclSuccess) { rtla_close(x); return RTLA_E_COMM; }
+    }
   }
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
@@ -557,10 +741,10 @@ static int allreduce2_u64(rtla_ctx* x, uint64_t* sum, int n1, uint64_t* mx, int 
   if (x->world == 1) return RTLA_OK;
   HIPCHK(hipMemcpyAsync(x->red, sum, 8 * n1, hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipMemcpyAsync(x->red + 32, mx, 8 * n2, hipMemcpyHostToDevice, x->stream));
-  NCCLCHK(ncclGroupStart());
-  NCCLCHK(ncclAllReduce(x->red, x->red, n1, ncclUint64, ncclSum, x->comm, x->stream));
-  NCCLCHK(ncclAllReduce(x->red + 32, x->red + 32, n2, ncclUint64, ncclMax, x->comm, x->stream));
-  NCCLCHK(ncclGroupEnd());
+  if (!x->shm) NCCLCHK(ncclGroupStart());
+  if (int rc = comm_allreduce(x, x->red, n1, 0)) return rc;
+  if (int rc = comm_allreduce(x, x->red + 32, n2, 1)) return rc;
+  if (!x->shm) NCCLCHK(ncclGroupEnd());
   HIPCHK(hipMemcpyAsync(sum, x->red, 8 * n1, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipMemcpyAsync(mx, x->red + 32, 8 * n2, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
@@ -571,7 +755,7 @@ static int allreduce2_u64(rtla_ctx* x, uint64_t* sum, int n1, uint64_t* mx, int 
 static int allreduce_u64(rtla_ctx* x, uint64_t* v, int n, int op) {
   if (x->world == 1) return RTLA_OK;
   HIPCHK(hipMemcpyAsync(x->red, v, 8 * n, hipMemcpyHostToDevice, x->stream));
-  NCCLCHK(ncclAllReduce(x->red, x->red, n, ncclUint64, op ? ncclMax : ncclSum, x->comm, x->stream));
+  if (int rc = comm_allreduce(x, x->red, n, op)) return rc;
   HIPCHK(hipMemcpyAsync(v, x->red, 8 * n, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   return RTLA_OK;
@@ -788,7 +972,7 @@ static int gather_counts(rtla_ctx* x) {
       for (auto& src : x->sh) dst.h_in[src.id] = src.h_out[dst.id];
   } else {
     Shard& s = x->sh[0];
-    NCCLCHK(ncclAllGather(s.out_count, s.all_count, G, ncclUint64, x->comm, x->stream));
+    if (int rc = comm_allgather(x, s.out_count, s.all_count, G)) return rc;
     HIPCHK(hipMemcpyAsync(s.h_all.data(), s.all_count, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
     HIPCHK(hipStreamSynchronize(x->stream));
     for (int p = 0; p < G; p++) {
@@ -823,14 +1007,13 @@ static int move_fps(rtla_ctx* x) {
     return RTLA_OK;
   }
   Shard& s = x->sh[0];
-  NCCLCHK(ncclGroupStart());
+  std::vector<Msg> sends, recvs;
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
-    if (s.h_out[p]) NCCLCHK(ncclSend(s.send_fp + 2 * (uint64_t)p * cap, 2 * s.h_out[p], ncclUint64, p, x->comm, x->stream));
-    if (s.h_in[p]) NCCLCHK(ncclRecv(s.recv_fp + 2 * (uint64_t)p * cap, 2 * s.h_in[p], ncclUint64, p, x->comm, x->stream));
+    if (s.h_out[p]) sends.push_back({s.send_fp + 2 * (uint64_t)p * cap, 16 * s.h_out[p], p});
+    if (s.h_in[p]) recvs.push_back({s.recv_fp + 2 * (uint64_t)p * cap, 16 * s.h_in[p], p});
   }
-  NCCLCHK(ncclGroupEnd());
-  return RTLA_OK;
+  return comm_exchange(x, sends, recvs);
 }
 
 // (2) Owners answered in recv_ans (0 = seen, 1 + rank = new): route the
@@ -854,14 +1037,14 @@ static int move_answers(rtla_ctx* x) {
     return RTLA_OK;
   }
   Shard& s = x->sh[0];
-  NCCLCHK(ncclGroupStart());
+  std::vector<Msg> sends, recvs;
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
-    if (s.h_in[p]) NCCLCHK(ncclSend(s.recv_ans + (uint64_t)p * cap, s.h_in[p], ncclUint32, p, x->comm, x->stream));
-    if (s.h_out[p]) NCCLCHK(ncclRecv(s.send_ans + (uint64_t)p * cap, s.h_out[p], ncclUint32, p, x->comm, x->stream));
+    if (s.h_in[p]) sends.push_back({s.recv_ans + (uint64_t)p * cap, 4 * s.h_in[p], p});
+    if (s.h_out[p]) recvs.push_back({s.send_ans + (uint64_t)p * cap, 4 * s.h_out[p], p});
   }
-  NCCLCHK(ncclGroupEnd());
-  NCCLCHK(ncclAllGather(s.new_count, s.all_new, G, ncclUint64, x->comm, x->stream));
+  if (int rc = comm_exchange(x, sends, recvs)) return rc;
+  if (int rc = comm_allgather(x, s.new_count, s.all_new, G)) return rc;
   HIPCHK(hipMemcpyAsync(s.h_all.data(), s.all_new, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   for (int p = 0; p < G; p++) {
@@ -902,15 +1085,14 @@ static int move_rows(rtla_ctx* x, uint64_t lo) {
     return RTLA_OK;
   }
   Shard& s = x->sh[0];
-  NCCLCHK(ncclGroupStart());
+  std::vector<Msg> sends, recvs;
   for (int p = 0; p < G; p++) {
     if (p == s.id) continue;
     const uint64_t no = part(s.h_new_out[p]), ni = part(s.h_new_in[p]);
-    if (no) NCCLCHK(ncclSend(s.send_rows + (uint64_t)p * rc * RW, no * RW, ncclUint32, p, x->comm, x->stream));
-    if (ni) NCCLCHK(ncclRecv(s.recv_rows + (uint64_t)p * rc * RW, ni * RW, ncclUint32, p, x->comm, x->stream));
+    if (no) sends.push_back({s.send_rows + (uint64_t)p * rc * RW, 4 * no * RW, p});
+    if (ni) recvs.push_back({s.recv_rows + (uint64_t)p * rc * RW, 4 * ni * RW, p});
   }
-  NCCLCHK(ncclGroupEnd());
-  return RTLA_OK;
+  return comm_exchange(x, sends, recvs);
 }
 
 // RTLA_STAMPS builds with RTLA_STAMPS_PRINT set: where the level kernel's
@@ -1154,7 +1336,7 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
     if (mn == 0) return RTLA_E_STATE;
     int root = (int)((uint64_t)x->nshard - mn);
     HIPCHK(hipMemcpyAsync(x->red, start, 32, hipMemcpyHostToDevice, x->stream));
-    NCCLCHK(ncclBroadcast(x->red, x->red, 4, ncclUint64, root, x->comm, x->stream));
+    if (int rc2 = comm_bcast(x, x->red, 4, root)) return rc2;
     HIPCHK(hipMemcpyAsync(start, x->red, 32, hipMemcpyDeviceToHost, x->stream));
     HIPCHK(hipStreamSynchronize(x->stream));
   } else if (!start[0]) {
@@ -1169,7 +1351,7 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
       HIPCHK(hipMemcpy(&p, x->sh[shard].parents + g, 8, hipMemcpyDeviceToHost));
     } else {
       if ((int)shard == x->rank) HIPCHK(hipMemcpyAsync(x->red, x->sh[0].parents + g, 8, hipMemcpyDeviceToDevice, x->stream));
-      NCCLCHK(ncclBroadcast(x->red, x->red, 1, ncclUint64, (int)shard, x->comm, x->stream));
+      if (int rc2 = comm_bcast(x, x->red, 1, (int)shard)) return rc2;
       HIPCHK(hipMemcpyAsync(&p, x->red, 8, hipMemcpyDeviceToHost, x->stream));
       HIPCHK(hipStreamSynchronize(x->stream));
     }

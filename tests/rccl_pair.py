@@ -1,5 +1,6 @@
-"""One rank of a world-size-N BFS over RCCL (test helper, run as a child
-process by test_gpu.py::test_rccl_ranks_match_golden): rank 0 writes the
+"""One rank of a world-size-N BFS (test helper, run as a child process by
+test_gpu.py::test_ranks_over_shm_transport_match_golden with
+RTLA_TRANSPORT=shm, or over RCCL by tools/gpu_rccl_pair.sh): rank 0 writes the
 RCCL unique id to a file, the other ranks poll for it -- the CLI's
 rendezvous -- then every rank runs the golden model and rank 0 prints the
 per-level counts as JSON.  Ranks share the device when the box has fewer
@@ -38,8 +39,9 @@ def main():
         while st == rtla.OK:
             st = ck.step()
         levels = [[lv.new, lv.generated] for lv in ck.levels]
+        trace = ck.trace() if st == rtla.VIOLATION else []  # collective: every rank walks it
         out = {"rank": rank, "levels": levels, "distinct": ck.distinct, "generated": ck.generated,
-               "status": st, "info": ck.device_info() if hasattr(ck, "device_info") else ""}
+               "status": st, "trace": trace, "info": ck.device_info()}
     print(json.dumps(out), flush=True)
 
 

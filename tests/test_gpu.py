@@ -617,6 +617,38 @@ def test_synthetic_step_dedup_counts():
     assert [(lv.generated, lv.probes, lv.new) for lv in got] == expect
 
 
+@pytest.mark.parametrize("name,world", [("n3_v1_t2_l1_m1", 2), ("n3_v1_t2_l1_m1", 3), ("n2_v1_t2_l1_m1_sym", 2),
+                                        ("n3_v1_t3_l1_m1_ntl", 2)])
+def test_ranks_over_shm_transport_match_golden(tmp_path, name, world):
+    """The world > 1 protocol (one process per rank: count all-gathers,
+    all-to-all-v of fingerprints / answers / rows, reductions, the trace's
+    cross-rank broadcasts) over the shared-memory transport, several ranks on
+    this one GPU (RCCL refuses two ranks per device): every rank reports the
+    golden per-level counts, and a counterexample trace of the golden length,
+    the same on every rank."""
+    import subprocess
+    import sys
+    g = GOLD[name]
+    env = dict(os.environ, RTLA_TRANSPORT="shm", RTLA_SHM_SLOT_MB="32")
+    idfile = str(tmp_path / "comm_id")
+    helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_pair.py")
+    procs = [subprocess.Popen([sys.executable, helper, str(r), str(world), idfile, name], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-2000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["levels"] == g["levels"], "rank %d" % o["rank"]
+        assert (o["distinct"], o["generated"]) == (g["distinct"], g["generated"])
+        assert '"world": %d' % world in o["info"]
+    if g["violated"]:
+        assert all(o["status"] == rtla.VIOLATION for o in outs)
+        assert all(len(o["trace"]) == g["trace_len"] for o in outs)
+        assert outs[0]["trace"] == outs[1]["trace"]
+
+
 def test_synthetic_resident_dedup_matches_step():
     """bench.py's configs[4] path: inputs generated into the row arena once
     (rtla_synthetic_generate), then dedup passes over resident row ranges

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-end GPU check: the -m gpu suite, smoke(), the default bench line.
-OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/round; rm -rf $OUT; mkdir -p $OUT
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/round; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
