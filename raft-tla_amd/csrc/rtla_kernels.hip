@@ -643,9 +643,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   unsigned long long res_ob = 0;
   unsigned long long dedup_new = 0;  // XF_DEDUP_ONLY: new fingerprints (uniform)
   unsigned long long s0 = 0;  // first state of the current group
-#ifdef RTLA_PFP_SHFL
-  FP pfp0{0, 0}, pfp{0, 0};
-#endif
 
   // One atomic reserves nb next-level slots.  Slots past next_cap are
   // dropped and flagged (the level is then reported incomplete).
@@ -699,11 +696,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     DeltaT<NS> d;  // (2)
     d.enabled = 0;
     if (act) compute_delta<NS>(L, rows + sl * W, inst, d);
-#ifdef RTLA_PFP_SHFL
-    const FP qfp{shfl_u64(pfp.a, sl), shfl_u64(pfp.b, sl)};
-#else
     const FP qfp = pfpl[sl];
-#endif
     FP cfp{0, 0};
     int bad = 0;
     if (act) {
@@ -826,15 +819,140 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     pend = false;
   };
 
+  // ---- one chunk: lane t evaluates ring entry done + t (tile row << 8 |
+  // instance).  The outcome -- whether and where it probes -- is kept for
+  // issue_probe(), which runs after the previous chunk's probes resolved.
+  bool nprobe = false;
+  unsigned long long nidx = 0;
+  FP ncf{0, 0};
+  int nowner = me;
+  uint32_t ninfo_new = 0;
+  auto eval_chunk = [&](int done, int cnt) {
+    const bool active = lane < cnt;
+    const int e = active ? ring[(done + lane) & (RING - 1)] : 0;
+    const int sl = e >> 8, inst = e & 255;
+    const uint32_t* prow = rows + sl * W;
+    const FP qfp = pfpl[sl];
+    std::conditional_t<SYM, DeltaT<NS>, DeltaFpT<NS>> d;
+    d.enabled = 0;
+    if (!(xflags & XF_NO_DELTA)) {
+      const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
+      const bool one_family = __ballot(active && inst_family(L, inst) != f0) == 0ull;
+      if (!one_family || (xflags & XF_GENERIC_DELTA)) {
+        if (active) compute_delta<NS>(L, prow, inst, d);
+      } else if (active) {
+        switch (f0) {  // one family in the whole chunk: its code only
+          case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
+          case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
+          case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
+          case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
+          case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
+          case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
+          case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
+          case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
+          case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
+          default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
+        }
+      }
+    }
+    bool en = d.enabled != 0;
+    if (en && d.err) {
+      set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
+      en = false;
+    }
+    my_gen += en ? 1u : 0u;
+    nprobe = false;
+    nidx = 0;
+    ncf = FP{0, 0};
+    nowner = me;
+    ninfo_new = (uint32_t)sl << 16 | (uint32_t)inst;
+    if (en && d.in_model) {
+      FP cfp;
+      if constexpr (SYM) cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
+      else
+        cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
+                                    : fp_add(qfp, delta_fp<NS>(L, prow, d));
+      const FP qfp0 = row_fp(prow);
+      if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
+        // seen-set key: the fingerprint, or under SYMMETRY the orbit key
+        FP key = cfp;
+        if constexpr (SYM) key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
+        nprobe = !(xflags & XF_NO_PROBE);
+        ncf = key;
+        nidx = key.a >> (64 - tlog2);
+        nowner = MULTI ? fp_owner(key, box.nshard) : me;
+      }
+    }
+    if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
+      const int code = en ? cover_code(L, inst, d.sub) : -1;
+      const unsigned long long em = __ballot(en);
+      if (em) {
+        const int c0 = __shfl(code, __builtin_ctzll(em));
+        const bool same = en && code == c0;
+        const int n0 = __popcll(__ballot(same));
+        if (lane == 0) atomicAdd(&cov[c0], (unsigned)n0);
+        if (en && !same) atomicAdd(&cov[code], 1u);
+      }
+    }
+    // out-of-model successors: checked, never stored (not in the
+    // synthetic microbench, whose random states are no model's)
+    int bad = 0;
+    if (en && !d.in_model && !(xflags & XF_DEDUP_ONLY))
+      bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+    if (claim_violation(ctr, bad, lane)) {
+      ctr->viol_parent = cur_base + s0 + sl;
+      ctr->viol_inst = inst;
+      ctr->viol_in_model = 0;
+      ctr->viol_child = ~0ull;
+    }
+  };
+  auto issue_probe = [&]() {
+    asm volatile("" ::: "memory");
+    issue_cas();
+    if (nprobe) {
+      my_probe++;
+      pend = true;
+      pf = ncf;
+      pinfo = ninfo_new;
+      unsigned long long* slotp = &((MULTI && nowner != me) ? sent : table)[nidx];
+      // load first: most successors are already in the set, and a plain
+      // load is cheaper than an atomic at the memory side; the CAS is
+      // only issued (at resolve time) when the home slot reads empty
+      pold = (xflags & XF_CAS_ONLY) ? atomicCAS(slotp, 0ull, ncf.b | 1ull)
+                                    : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    nprobe = false;
+  };
+  // Append the pairs of instance q (bit q of this window's wave-wide mask)
+  // to the ring, Receive grouped by message type (one handler of
+  // raft.tla:421-436 per run).
+  auto append_instance = [&](int& pos, unsigned long long mask, int wb, int q, const uint32_t* prow_mine, int f) {
+    const bool mine = (mask >> q) & 1ull;
+    if (f == F_RECEIVE) {
+      const uint32_t ty = mine ? m_type(bag_slot(L, prow_mine, wb + q - L.fam[F_RECEIVE])) : 0u;
+#pragma unroll
+      for (uint32_t t = 0; t < 4; t++) {
+        const bool b = mine && ty == t;
+        const unsigned long long m = __ballot(b);
+        if (b) ring[(pos + __popcll(m & lanes_below)) & (RING - 1)] = (uint16_t)(lane << 8 | (wb + q));
+        pos += __popcll(m);
+      }
+    } else {
+      const unsigned long long m = __ballot(mine);
+      if (mine) ring[(pos + __popcll(m & lanes_below)) & (RING - 1)] = (uint16_t)(lane << 8 | (wb + q));
+      pos += __popcll(m);
+    }
+  };
+
   // Groups are handed out by a device-wide counter (one atomic per group,
   // the next one requested while the current group is processed): a wave
   // that became resident late, or drew heavy groups, simply takes fewer --
   // no static partition, no tail.  (The occupancy API can over-report the
   // resident blocks by one per CU; a static stride would then serialise 1/k
   // of the work behind the rest.)
-  const unsigned long long ngroups = (s_end - s_begin + GROUP - 1) / GROUP;
   unsigned long long gnext = 0;
   if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
+  const unsigned long long ngroups = (s_end - s_begin + GROUP - 1) / GROUP;
   for (unsigned long long gi = shfl0_u64(gnext); gi < ngroups; gi = shfl0_u64(gnext)) {
     if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
     s0 = s_begin + gi * GROUP;
@@ -850,12 +968,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     const uint32_t* prow_mine = rows + (lane & (GROUP - 1)) * W;
     int nmsg = 0;
     if (valid) {
-#ifdef RTLA_PFP_SHFL
-      pfp0 = row_fp(prow_mine);
-      pfp = fp_add(pfp0, alllogs_delta<NS>(L, prow_mine, pall_mine));
-#else
       pfpl[lane] = fp_add(row_fp(prow_mine), alllogs_delta<NS>(L, prow_mine, pall_mine));
-#endif
       if (SYM) afpl[lane] = alllogs_fp(L, pall_mine);
       nmsg = row_nmsg(L, prow_mine);
     }
@@ -864,121 +977,24 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     for (int wb = 0; wb < ((xflags & XF_NO_CHUNKS) ? 0 : ninst); wb += 64) {
       const unsigned long long mask = valid ? cand_mask<NS>(L, prow_mine, nmsg, wb) : 0ull;
       unsigned long long todo = wave_or_u64(mask);
-      int pos = 0, done = 0, cfam = -1;
+      int pos = 0, done = 0;
       while (todo || pos > done) {
         // Append the pairs of the next instance(s) until a chunk is ready.  A
         // chunk is cut at a family boundary once it is a third full, so most
-        // chunks hold one family and take the specialised path below.
+        // chunks hold one family and take the specialised path.
+        int cfam = -1;
         while (todo && pos - done < 64) {
           const int q = __builtin_ctzll(todo);
           const int f = inst_family(L, wb + q);
           if (f != cfam && pos - done >= 22) break;
           cfam = f;
           todo &= todo - 1;
-          const bool mine = (mask >> q) & 1ull;
-          if (f == F_RECEIVE) {  // group by message type: one handler of raft.tla:421-436 per run
-            const uint32_t ty = mine ? m_type(bag_slot(L, prow_mine, wb + q - L.fam[F_RECEIVE])) : 0u;
-#pragma unroll
-            for (uint32_t t = 0; t < 4; t++) {
-              const bool b = mine && ty == t;
-              const unsigned long long m = __ballot(b);
-              if (b) ring[(pos + __popcll(m & lanes_below)) & (RING - 1)] = (uint16_t)(lane << 8 | q);
-              pos += __popcll(m);
-            }
-          } else {
-            const unsigned long long m = __ballot(mine);
-            if (mine) ring[(pos + __popcll(m & lanes_below)) & (RING - 1)] = (uint16_t)(lane << 8 | q);
-            pos += __popcll(m);
-          }
+          append_instance(pos, mask, wb, q, prow_mine, f);
         }
-        cfam = -1;
         const int cnt = min(64, pos - done);
         wave_sync();
         STAMP(1);  // pair ring
-        // ---- one chunk: lane t evaluates pair done + t
-        const bool active = lane < cnt;
-        const int e = active ? ring[(done + lane) & (RING - 1)] : 0;
-        const int sl = e >> 8, inst = wb + (e & 255);
-        const uint32_t* prow = rows + sl * W;
-#ifdef RTLA_PFP_SHFL
-        const FP qfp{shfl_u64(pfp.a, sl), shfl_u64(pfp.b, sl)};
-        const FP qfp0{shfl_u64(pfp0.a, sl), shfl_u64(pfp0.b, sl)};
-#else
-        const FP qfp = pfpl[sl];
-#endif
-        std::conditional_t<SYM, DeltaT<NS>, DeltaFpT<NS>> d;
-        d.enabled = 0;
-        if (!(xflags & XF_NO_DELTA)) {
-          const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
-          const int f1 = inst_family(L, __builtin_amdgcn_readlane(inst, cnt - 1));
-          if (f0 != f1 || (xflags & XF_GENERIC_DELTA)) {
-            if (active) compute_delta<NS>(L, prow, inst, d);
-          } else if (active) {
-            switch (f0) {  // one family in the whole chunk: its code only
-              case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
-              case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
-              case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
-              case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
-              case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
-              case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
-              case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
-              case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
-              case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
-              default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
-            }
-          }
-        }
-        bool en = d.enabled != 0;
-        if (en && d.err) {
-          set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
-          en = false;
-        }
-        my_gen += en ? 1u : 0u;
-        bool probe = false;
-        unsigned long long idx = 0;
-        FP cf{0, 0};
-        int owner = me;
-        if (en && d.in_model) {
-          FP cfp;
-          if constexpr (SYM) cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
-          else
-            cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
-                                        : fp_add(qfp, delta_fp<NS>(L, prow, d));
-#ifndef RTLA_PFP_SHFL
-          const FP qfp0 = row_fp(prow);
-#endif
-          if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
-            // seen-set key: the fingerprint, or under SYMMETRY the orbit key
-            FP key = cfp;
-            if constexpr (SYM) key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
-            probe = !(xflags & XF_NO_PROBE);
-            cf = key;
-            idx = key.a >> (64 - tlog2);
-            owner = MULTI ? fp_owner(key, box.nshard) : me;
-          }
-        }
-        if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
-          const int code = en ? cover_code(L, inst, d.sub) : -1;
-          const unsigned long long em = __ballot(en);
-          if (em) {
-            const int c0 = __shfl(code, __builtin_ctzll(em));
-            const bool same = en && code == c0;
-            const int n0 = __popcll(__ballot(same));
-            if (lane == 0) atomicAdd(&cov[c0], (unsigned)n0);
-            if (en && !same) atomicAdd(&cov[code], 1u);
-          }
-        }
-        // out-of-model successors: checked, never stored (not in the
-        // synthetic microbench, whose random states are no model's)
-        int bad = 0;
-        if (en && !d.in_model && !(xflags & XF_DEDUP_ONLY))
-          bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-        if (claim_violation(ctr, bad, lane)) {
-          ctr->viol_parent = cur_base + s0 + sl;
-          ctr->viol_inst = inst;
-          ctr->viol_in_model = 0;
-          ctr->viol_child = ~0ull;
-        }
+        eval_chunk(done, cnt);
         STAMP(2);  // successor deltas, fingerprints, coverage, out-of-model invariants
         resolve();  // the previous chunk's probes, after this chunk's arithmetic
         STAMP(3);
@@ -995,20 +1011,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           res_ob = reserve_issue(64);
           have_res = true;
         }
-        asm volatile("" ::: "memory");
-        issue_cas();
-        if (probe) {
-          my_probe++;
-          pend = true;
-          pf = cf;
-          pinfo = (uint32_t)sl << 16 | (uint32_t)inst;
-          unsigned long long* slotp = &((MULTI && owner != me) ? sent : table)[idx];
-          // load first: most successors are already in the set, and a plain
-          // load is cheaper than an atomic at the memory side; the CAS is
-          // only issued (at resolve time) when the home slot reads empty
-          pold = (xflags & XF_CAS_ONLY) ? atomicCAS(slotp, 0ull, cf.b | 1ull)
-                                        : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        issue_probe();
         STAMP(4);  // slot reservation, probe issue
         done += cnt;
       }
