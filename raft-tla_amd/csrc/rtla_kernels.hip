@@ -964,6 +964,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       if (RTLA_IDX_OK(ctr, ring_idx(cur, s0) + nvalid, cur.cap + 1)) copy_words_lds16(rows, src, nw, lane);
     }
     wave_sync();
+    // the next group's number (its atomic returned before the tile copy's wait)
+    const unsigned long long gnn = shfl0_u64(gnext);
     const bool valid = lane < nvalid;
     const uint32_t* prow_mine = rows + (lane & (GROUP - 1)) * W;
     int nmsg = 0;
@@ -1018,6 +1020,19 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     }
     // Group end: the last probes and every pending row (their parents are
     // this group's rows, which the next group overwrites).
+    // Touch every 128-byte line of the next group's rows now, so that its
+    // tile load after this drain hits the caches.  (Loads in inline asm: the
+    // compiler neither drops them nor tracks them; its own waits can only
+    // over-wait because of them, and the drain's end waits for them.)
+    uint32_t pfa = 0, pfb = 0;
+    if (gnn < ngroups) {
+      const unsigned long long sn = s_begin + gnn * GROUP;
+      const int lines = ((int)min<unsigned long long>((unsigned long long)GROUP, s_end - sn) * W + 31) / 32;
+      const uint32_t* pa = ring_row(cur, sn, W) + 32 * min(lane, lines - 1);
+      const uint32_t* pb = ring_row(cur, sn, W) + 32 * min(lane + 64, lines - 1);
+      asm volatile("global_load_dword %0, %1, off" : "=v"(pfa) : "v"(pa) : "memory");
+      asm volatile("global_load_dword %0, %1, off" : "=v"(pfb) : "v"(pb) : "memory");
+    }
     resolve();
     if (async_cas) {  // the CAS this resolve set up, then its result
       issue_cas();
@@ -1031,6 +1046,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       const int nb = min(64, tail - head);
       build_rows(reserve_take(reserve_issue(nb), nb), nb);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::"v"(pfa), "v"(pfb));
     wave_sync();
     STAMP(6);  // group-end drain
   }
