@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 5
+#define RTLA_ABI_VERSION 6
 
 /* status codes */
 #define RTLA_OK 0
@@ -151,6 +151,17 @@ int rtla_init_row(const rtla_cfg *cfg, uint32_t *row);
 int rtla_expand_batch(const rtla_cfg *cfg, const uint32_t *rows, size_t n, uint32_t *succ,
                       uint64_t *info, size_t cap, size_t *n_out);
 int rtla_state_text(const rtla_cfg *cfg, const uint32_t *row, char *buf, size_t cap);
+/* Level digests for parity: *out = sum (mod 2^64) over the rows of FNV-1a-64 of
+ * rtla_state_text -- an order-free digest of a SET of states, the quantity the
+ * CPU oracle records per BFS level (oracle/raft_cpu.c level_text_hash; TLC has
+ * no counterpart: it is how TLC's per-level state sets are compared here).
+ * threads: host threads (0 = the process's CPU allowance, at most 16).
+ * rtla_level_text_hash digests the current frontier (the level last produced)
+ * of the whole job: device rows are streamed to the host in chunks, every
+ * local shard is included, and with world > 1 it is collective (summed over
+ * ranks). */
+int rtla_rows_text_hash(const rtla_cfg *cfg, const uint32_t *rows, size_t n, int threads, uint64_t *out);
+int rtla_level_text_hash(rtla_ctx *ctx, int threads, uint64_t *out);
 int rtla_action_name(const rtla_cfg *cfg, int32_t inst, int32_t sub, char *buf, size_t cap);
 int rtla_invariants(const rtla_cfg *cfg, const uint32_t *row);  /* violated mask */
 /* Fingerprint of a row recomputed from scratch (the kernels derive it

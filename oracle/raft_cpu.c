@@ -837,6 +837,8 @@ typedef struct {
     uint64_t level_base;
     int check_text_hash;
     uint64_t *text_hash; /* per thread */
+    int count_only;      /* the last level of a max_levels prefix: count new states, keep none */
+    uint64_t *nnew;      /* per thread: new states of the level */
 } Bfs;
 
 typedef struct { Bfs *b; int tid; uint64_t parent_idx; uint8_t *ser; } EmitCtx;
@@ -859,7 +861,9 @@ static void bfs_emit(void *ud, const State *t, int action, int arg) {
         if (!b->c->symmetry) hash128(e->ser, len, &h1, &h2);
         isnew = seen_put(b->seen, h1, h2);
         if (isnew) {
-            arena_push(&b->outs[e->tid], e->ser, len, e->parent_idx, (uint32_t)(action << 16 | arg));
+            b->nnew[e->tid]++;
+            if (!b->count_only)
+                arena_push(&b->outs[e->tid], e->ser, len, e->parent_idx, (uint32_t)(action << 16 | arg));
             if (b->check_text_hash) {
                 char *tx = state_text(b->c, t);
                 b->text_hash[e->tid] += orc_text_hash(tx);
@@ -924,6 +928,7 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
     b.gen = (uint64_t *)calloc((size_t)nthreads, 8);
     b.cover = (uint64_t *)calloc((size_t)nthreads * A_COUNT, 8);
     b.text_hash = (uint64_t *)calloc((size_t)nthreads, 8);
+    b.nnew = (uint64_t *)calloc((size_t)nthreads, 8);
 
     /* all levels (kept only when tracing) */
     Arena *levels = (Arena *)calloc(ORC_MAX_LEVELS + 1, sizeof(Arena));
@@ -950,13 +955,15 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
         atomic_store(&b.next_item, 0);
         memset(b.gen, 0, 8 * (size_t)nthreads);
         memset(b.text_hash, 0, 8 * (size_t)nthreads);
+        memset(b.nnew, 0, 8 * (size_t)nthreads);
+        b.count_only = c->max_levels > 0 && r->n_levels + 1 >= c->max_levels && !keep_trace;
         pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
         EmitCtx *ecs = (EmitCtx *)calloc((size_t)nthreads, sizeof(EmitCtx));
         for (int k = 0; k < nthreads; k++) { ecs[k].b = &b; ecs[k].tid = k; pthread_create(&th[k], NULL, bfs_worker, &ecs[k]); }
         for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
         free(th); free(ecs);
         uint64_t gen = 0, nnew = 0, th_sum = 0;
-        for (int k = 0; k < nthreads; k++) { gen += b.gen[k]; nnew += b.outs[k].cnt; th_sum += b.text_hash[k]; }
+        for (int k = 0; k < nthreads; k++) { gen += b.gen[k]; nnew += b.nnew[k]; th_sum += b.text_hash[k]; }
         r->generated += gen;
         r->distinct += nnew;
         if (g_overflow) { rc = ORC_E_OVERFLOW; break; }
@@ -974,7 +981,7 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
                 size_t l2 = (q + 1 < a->cnt ? a->off[q + 1] : a->n) - a->off[q];
                 arena_push(nx, a->buf + a->off[q], l2, a->parent[q], a->act[q]);
             }
-            a->n = 0; a->cnt = 0;
+            arena_free(a);
         }
         for (size_t q = 0; q < nx->cnt; q++) {
             size_t l2 = (q + 1 < nx->cnt ? nx->off[q + 1] : nx->n) - nx->off[q];
@@ -991,6 +998,7 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
         }
         if (nnew == 0) break;
         if (c->max_distinct && r->distinct > c->max_distinct) { rc = ORC_E_BUDGET; break; }
+        if (c->max_levels && r->n_levels >= c->max_levels) { rc = ORC_E_BUDGET; break; }
     }
     r->depth = 0;
     for (int L = 0; L < r->n_levels; L++) if (r->level_new[L]) r->depth = L + 1;
@@ -1037,7 +1045,7 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
     for (int L = 0; L <= cur && L <= ORC_MAX_LEVELS; L++) arena_free(&levels[L]);
     free(levels); free(level_base);
     for (int k = 0; k < nthreads; k++) arena_free(&b.outs[k]);
-    free(b.outs); free(b.gen); free(b.cover); free(b.text_hash);
+    free(b.outs); free(b.gen); free(b.cover); free(b.text_hash); free(b.nnew);
     free(b.v_state);
     seen_free(b.seen);
     free(s0); free(ser);

@@ -23,7 +23,9 @@ typedef struct {
     int max_msgs;           /* 0 = unbounded; else BagCardinality(messages) <= max_msgs */
     uint64_t max_distinct;  /* 0 = unlimited; stop with ORC_E_BUDGET beyond */
     int symmetry;           /* SYMMETRY Permutations(Server): count server-permutation orbits */
-    int pad_;
+    int max_levels;         /* 0 = unlimited; else stop after this many levels (Init = 1).  The last
+                               level's new states are counted, hashed and deduplicated but not kept,
+                               so a prefix reaches one level further in the same memory */
 } orc_cfg;
 
 typedef struct {

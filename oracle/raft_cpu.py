@@ -20,7 +20,7 @@ class OrcCfg(C.Structure):
     _fields_ = [("n_server", C.c_int), ("n_value", C.c_int), ("max_term", C.c_int),
                 ("max_log", C.c_int), ("max_copies", C.c_int), ("inv_mask", C.c_int),
                 ("verbose", C.c_int), ("max_msgs", C.c_int), ("max_distinct", C.c_uint64),
-                ("symmetry", C.c_int), ("pad_", C.c_int)]
+                ("symmetry", C.c_int), ("max_levels", C.c_int)]
 
 
 class OrcResult(C.Structure):
@@ -63,11 +63,11 @@ def lib():
 
 
 def cfg_of(n_server, n_value, max_term, max_log, max_copies, max_msgs=0, invariants=(),
-           max_distinct=0, symmetry=False):
+           max_distinct=0, symmetry=False, max_levels=0):
     m = 0
     for n in invariants:
         m |= INV[n]
-    return OrcCfg(n_server, n_value, max_term, max_log, max_copies, m, 0, max_msgs, max_distinct, int(symmetry), 0)
+    return OrcCfg(n_server, n_value, max_term, max_log, max_copies, m, 0, max_msgs, max_distinct, int(symmetry), max_levels)
 
 
 def bfs(cfg: OrcCfg, threads=8, keep_trace=False, text_hash=False):

@@ -20,6 +20,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(a, "-w")) { threads = atoi(v); i++; }
         else if (!strcmp(a, "-m")) { c.max_distinct = strtoull(v, 0, 10); i++; }
         else if (!strcmp(a, "-s")) { c.symmetry = 1; }
+        else if (!strcmp(a, "-L")) { c.max_levels = atoi(v); i++; }
         else if (!strcmp(a, "--trace")) trace = 1;
         else if (!strcmp(a, "-q")) c.verbose = 0;
         else { fprintf(stderr, "unknown arg %s\n", a); return 2; }

@@ -17,6 +17,8 @@
 // 12 = safety violation, 150/151 = spec/config errors, 255 = other errors
 // (TLC's ExitStatus values as we understand them; not verified against a
 // live TLC here).
+#include <errno.h>
+#include <signal.h>
 #include <spawn.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -246,13 +248,48 @@ int launch_ranks(int n, char** argv) {
     }
     pids.push_back(pid);
   }
-  int code0 = 0, worst = 0;
-  for (int r = 0; r < n; r++) {
+  // Reap ranks in whatever order they end.  A rank killed by a signal, or
+  // ending with an error status other than the ones every rank reaches
+  // together (0, 12 = invariant violated, 150/151 = spec/cfg errors), may
+  // leave the others blocked in a collective: they get a grace period to end
+  // on their own, then SIGTERM, then SIGKILL.  No rank is ever restarted.
+  int code0 = 0, worst = 0, left = n;
+  std::vector<bool> done(n, false);
+  double abort_at = -1.0;  // monotonic seconds at which the survivors are terminated
+  bool termed = false;
+  auto now = []() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+  };
+  while (left > 0) {
     int st = 0;
-    waitpid(pids[r], &st, 0);
-    const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 255;
-    if (r == 0) code0 = code;
-    else if (code && !worst) worst = code;
+    const pid_t pid = waitpid(-1, &st, WNOHANG);
+    if (pid > 0) {
+      int r = 0;
+      while (r < n && pids[r] != pid) r++;
+      if (r == n || done[r]) continue;
+      done[r] = true;
+      left--;
+      const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 255;
+      if (r == 0) code0 = code;
+      else if (code && !worst) worst = code;
+      const bool abnormal = !WIFEXITED(st) || (code != 0 && code != 12 && code != 150 && code != 151);
+      if (abnormal && abort_at < 0 && left > 0) {
+        fprintf(stderr, "rtla: rank %d ended abnormally (%s %d); stopping the other ranks in 10 s\n", r,
+                WIFEXITED(st) ? "exit status" : "signal", WIFEXITED(st) ? code : WTERMSIG(st));
+        abort_at = now() + 10.0;
+      }
+      continue;
+    }
+    if (pid < 0 && errno != EINTR) break;
+    if (abort_at >= 0 && now() > abort_at) {
+      for (int r = 0; r < n; r++)
+        if (!done[r]) kill(pids[r], termed ? SIGKILL : SIGTERM);
+      abort_at = now() + 5.0;
+      termed = true;
+    }
+    usleep(20000);
   }
   (void)remove(rdv.c_str());
   (void)rmdir(dir);
@@ -553,10 +590,13 @@ int main(int argc, char** argv) {
     printf("  Estimates of the probability that TLC did not check all reachable states\n"
            "  because two distinct states had the same fingerprint:\n"
            "  calculated (optimistic):  val = %.1E\n",
-           // The set stores 63 bits of the fingerprint (fp.b | 1) at a slot
-           // chosen by fp.a; a probe walks ~2 slots at the loads used, so
-           // each generated state is compared with ~2 random 63-bit keys.
-           (double)ls.generated_total * 2.0 / 9.223372036854775808e18);
+           // TLC's formula (distinct x (generated - distinct) / 2^64), kept so
+           // tools that parse this line read the quantity TLC reports
+           (double)ls.distinct_total * (double)(ls.generated_total - ls.distinct_total) / 1.8446744073709552e19);
+    // this checker's own estimate: the set stores 63 key bits (fp.b | 1) at
+    // a slot chosen by fp.a; a probe compares each generated state with ~2
+    // random keys at the loads used
+    printf("  rtla 63-bit-key estimate:  val = %.1E\n", (double)ls.generated_total * 2.0 / 9.223372036854775808e18);
   }
   if (coverage) {
     uint64_t g[16], d[16];

@@ -48,6 +48,7 @@
 #include <chrono>
 #include <cstdio>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rtla.h"
@@ -442,6 +443,82 @@ extern "C" int rtla_action_name(const rtla_cfg* c, int32_t inst, int32_t sub, ch
   return (int)s.size();
 }
 
+// ---- level digests (rtla_rows_text_hash / rtla_level_text_hash): the sum of
+// FNV-1a-64 of each state's canonical text, computed by a pool of host threads.
+static int text_threads(int want) {
+  if (want > 0) return std::min(want, 256);
+  int n = 0;
+  if (const char* e = getenv("OMP_NUM_THREADS")) n = atoi(e);  // the GPU box's per-job CPU allowance
+  if (n <= 0) {
+    cpu_set_t cs;
+    n = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : 8;
+  }
+  return std::max(1, std::min(n, 16));
+}
+
+// FNV-1a is one serial multiply chain per text: 8 texts are hashed together
+// so the chains overlap (multiplier throughput, not latency, bounds a core).
+constexpr int TEXT_ILP = 8;
+static uint64_t fnv1a64_sum(char* const* txt, const size_t* len, int m) {
+  uint64_t h[TEXT_ILP];
+  size_t common = ~(size_t)0;
+  for (int i = 0; i < m; i++) {
+    h[i] = 0xcbf29ce484222325ull;
+    common = std::min(common, len[i]);
+  }
+  for (size_t k = 0; k < common; k++)
+    for (int i = 0; i < TEXT_ILP; i++)
+      if (i < m) h[i] = (h[i] ^ (unsigned char)txt[i][k]) * 0x100000001b3ull;
+  uint64_t sum = 0;
+  for (int i = 0; i < m; i++) {
+    for (size_t k = common; k < len[i]; k++) h[i] = (h[i] ^ (unsigned char)txt[i][k]) * 0x100000001b3ull;
+    sum += h[i];
+  }
+  return sum;
+}
+
+static uint64_t rows_digest(const Layout& L, const uint32_t* rows, size_t n, int threads) {
+  threads = (int)std::min<size_t>((size_t)threads, std::max<size_t>(1, n / 4096));
+  std::vector<uint64_t> part((size_t)threads, 0);
+  std::atomic<size_t> next{0};
+  const size_t cap = state_text_cap(L);
+  auto work = [&](int t) {
+    std::vector<char> buf((TEXT_ILP + 1) * cap);  // TEXT_ILP texts + one scratch area
+    char* txt[TEXT_ILP];
+    size_t len[TEXT_ILP];
+    for (int i = 0; i < TEXT_ILP; i++) txt[i] = buf.data() + i * cap;
+    char* scratch = buf.data() + TEXT_ILP * cap;
+    uint64_t acc = 0;
+    for (;;) {
+      const size_t b = next.fetch_add(8192);
+      if (b >= n) break;
+      const size_t e = std::min(n, b + 8192);
+      for (size_t k = b; k < e; k += TEXT_ILP) {
+        const int m = (int)std::min<size_t>(TEXT_ILP, e - k);
+        for (int i = 0; i < m; i++) len[i] = state_text_into(L, rows + (k + i) * (size_t)L.W, txt[i], scratch);
+        acc += fnv1a64_sum(txt, len, m);
+      }
+    }
+    part[(size_t)t] = acc;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; t++) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  uint64_t sum = 0;
+  for (uint64_t v : part) sum += v;
+  return sum;
+}
+
+extern "C" int rtla_rows_text_hash(const rtla_cfg* c, const uint32_t* rows, size_t n, int threads, uint64_t* out) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  if (!out || (n && !rows)) return RTLA_E_ARG;
+  *out = rows_digest(L, rows, n, text_threads(threads));
+  return RTLA_OK;
+}
+
 static int flags_to_status(int flags) {
   if (flags & FLAG_SPEC_ERROR) return RTLA_E_SPEC;
   if (flags) return RTLA_E_OVERFLOW;
@@ -810,17 +887,19 @@ std::string ckpt_path(const char* prefix, int shard) {
 }
 }  // namespace
 
+// Collective when world > 1: every rank reaches every reduction below, also
+// after a local failure (its flag travels in the reduction), so one rank's
+// error is every rank's error and no rank is left waiting in a collective.
 extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
   if (!x || !prefix) return RTLA_E_ARG;
   if (!x->inited) return RTLA_E_STATE;
-  HIPCHK(hipSetDevice(x->device));
-  HIPCHK(hipStreamSynchronize(x->stream));
   std::vector<char> buf(64 << 20);
   // Each shard is written to <path>.tmp (flushed to disk); only when every
   // shard of every rank has been written are the files renamed over the
   // previous checkpoint, so a crash mid-write leaves the last good one intact.
-  uint64_t failed = 0;
+  uint64_t failed = hipSetDevice(x->device) != hipSuccess || hipStreamSynchronize(x->stream) != hipSuccess ? 1 : 0;
   for (auto& s : x->sh) {
+    if (failed) break;
     CkptHeader h;
     memset(&h, 0, sizeof h);
     memcpy(h.magic, "RTLACKP1", 8);
@@ -844,27 +923,35 @@ extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
     ok = fclose(f) == 0 && ok;
     if (!ok) { failed = 1; break; }
   }
-  int rc = allreduce_u64(x, &failed, 1, 1);
-  if (rc) return rc;
+  if (int rc = allreduce_u64(x, &failed, 1, 1)) return rc;
   if (failed) {
     for (auto& s : x->sh) (void)remove((ckpt_path(prefix, s.id) + ".tmp").c_str());
     return RTLA_E_ARG;
   }
+  // the renames are agreed on too: every rank reports the same outcome
+  uint64_t renamed_bad = 0;
   for (auto& s : x->sh) {
     const std::string path = ckpt_path(prefix, s.id);
-    if (rename((path + ".tmp").c_str(), path.c_str()) != 0) return RTLA_E_ARG;
+    if (rename((path + ".tmp").c_str(), path.c_str()) != 0) renamed_bad = 1;
+  }
+  if (int rc = allreduce_u64(x, &renamed_bad, 1, 1)) return rc;
+  if (renamed_bad) {
+    fprintf(stderr, "rtla: checkpoint %s: a shard file could not be renamed into place "
+                    "(the checkpoint mixes generations; recover will refuse it)\n", prefix);
+    return RTLA_E_ARG;
   }
   return RTLA_OK;
 }
 
 extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
   if (!x || !prefix) return RTLA_E_ARG;
-  HIPCHK(hipSetDevice(x->device));
   std::vector<char> buf(64 << 20);
   int level = -1;
+  int err = hipSetDevice(x->device) != hipSuccess ? RTLA_E_HIP : RTLA_OK;  // the first local failure
   for (auto& s : x->sh) {
+    if (err) break;
     FILE* f = fopen(ckpt_path(prefix, s.id).c_str(), "rb");
-    if (!f) return RTLA_E_ARG;
+    if (!f) { err = RTLA_E_ARG; break; }
     CkptHeader h;
     bool ok = read_all(f, &h, sizeof h) && memcmp(h.magic, "RTLACKP1", 8) == 0 && h.abi == RTLA_ABI_VERSION &&
               h.nshard == x->nshard && h.shard == s.id && h.W == x->L.W && h.tlog2 == x->tlog2 &&
@@ -877,8 +964,8 @@ extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
          file_to_dev(f, s.parents, 8 * h.parents_n, buf) &&
          file_to_dev(f, s.arena, 4ull * x->L.W * h.n_cur, buf) && read_all(f, c.cover, sizeof c.cover);
     fclose(f);
-    if (!ok) return RTLA_E_STATE;
-    HIPCHK(hipMemcpy(s.ctr, &c, sizeof c, hipMemcpyHostToDevice));
+    if (!ok) { err = RTLA_E_STATE; break; }
+    if (hipMemcpy(s.ctr, &c, sizeof c, hipMemcpyHostToDevice) != hipSuccess) { err = RTLA_E_HIP; break; }
     level = h.level;
     s.cur_start = 0; s.cur_base = h.cur_base; s.n_cur = h.n_cur;
     s.viol_mask = h.viol_mask; s.viol_in_model = h.viol_in_model; s.viol_inst = h.viol_inst;
@@ -887,13 +974,20 @@ extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
     x->finished = h.finished != 0;
   }
   if (x->world > 1) {  // every rank must resume from the same level of the same search
-    uint64_t v[6] = {(uint64_t)x->level, x->distinct, x->generated, ~(uint64_t)x->level, ~x->distinct, ~x->generated};
-    int rc = allreduce_u64(x, v, 6, 1);
-    if (rc) return rc;
+    uint64_t v[7] = {(uint64_t)x->level, x->distinct, x->generated, ~(uint64_t)x->level, ~x->distinct, ~x->generated,
+                     err ? 1ull : 0ull};
+    if (int rc = allreduce_u64(x, v, 7, 1)) return rc;
+    if (err) return err;
+    if (v[6]) {
+      fprintf(stderr, "rtla: recover failed on another rank\n");
+      return RTLA_E_STATE;
+    }
     if (v[0] != ~v[3] || v[1] != ~v[4] || v[2] != ~v[5]) {
       fprintf(stderr, "rtla: checkpoint files of different ranks are from different levels\n");
       return RTLA_E_STATE;
     }
+  } else if (err) {
+    return err;
   }
   x->init_row.assign(x->L.W, 0);
   row_init(x->L, x->init_row.data());
@@ -1284,6 +1378,54 @@ extern "C" int rtla_frontier(rtla_ctx* x, uint32_t* rows, size_t cap, size_t* n)
       HIPCHK(ring_copy(cur_ring(x, s), x->L.W, 0, s.n_cur, rows + off * x->L.W, true));
     off += s.n_cur;
   }
+  return RTLA_OK;
+}
+
+// Digest of the current frontier: rows stream to the host in chunks (the
+// next chunk's copy overlaps the current chunk's hashing).
+extern "C" int rtla_level_text_hash(rtla_ctx* x, int threads, uint64_t* out) {
+  if (!x || !out) return RTLA_E_ARG;
+  if (!x->inited) return RTLA_E_STATE;
+  HIPCHK(hipSetDevice(x->device));
+  const int W = x->L.W;
+  const int nt = text_threads(threads);
+  const uint64_t CH = std::max<uint64_t>(1, (256ull << 20) / (4ull * W));  // ~256 MB of rows per chunk
+  uint32_t* hbuf[2] = {nullptr, nullptr};
+  for (auto& b : hbuf) HIPCHK(hipHostMalloc((void**)&b, CH * W * 4, hipHostMallocDefault));
+  uint64_t sum = 0;
+  int rc = RTLA_OK;
+  for (auto& s : x->sh) {
+    const Ring r = cur_ring(x, s);
+    // chunk j covers states [j * CH, ...); copies go in pieces that do not wrap the ring
+    auto issue = [&](uint64_t g0, uint32_t* dst) -> hipError_t {
+      uint64_t n = std::min<uint64_t>(CH, s.n_cur - g0), g = g0;
+      while (n) {
+        const uint64_t p = ring_idx(r, g), m = std::min<uint64_t>(n, r.cap - p);
+        hipError_t e = hipMemcpyAsync(dst, r.base + p * (uint64_t)W, m * W * 4, hipMemcpyDeviceToHost, x->stream);
+        if (e != hipSuccess) return e;
+        dst += m * (uint64_t)W;
+        g += m;
+        n -= m;
+      }
+      return hipSuccess;
+    };
+    if (!s.n_cur) continue;
+    if (issue(0, hbuf[0]) != hipSuccess) { rc = RTLA_E_HIP; break; }
+    for (uint64_t g = 0, j = 0; g < s.n_cur; g += CH, j++) {
+      if (hipStreamSynchronize(x->stream) != hipSuccess) { rc = RTLA_E_HIP; break; }
+      if (g + CH < s.n_cur && issue(g + CH, hbuf[(j + 1) & 1]) != hipSuccess) { rc = RTLA_E_HIP; break; }
+      sum += rows_digest(x->L, hbuf[j & 1], std::min<uint64_t>(CH, s.n_cur - g), nt);
+    }
+    if (rc) break;
+  }
+  (void)hipStreamSynchronize(x->stream);
+  for (auto& b : hbuf) (void)hipHostFree(b);
+  // every rank joins the reduction, also after a local failure (the flag travels with it)
+  uint64_t v[2] = {sum, rc ? 1ull : 0ull};
+  if (int e = allreduce_u64(x, v, 2, 0)) return e;
+  if (rc) return rc;
+  if (v[1]) return RTLA_E_HIP;
+  *out = v[0];
   return RTLA_OK;
 }
 

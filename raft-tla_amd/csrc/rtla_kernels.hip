@@ -1021,17 +1021,20 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     // Group end: the last probes and every pending row (their parents are
     // this group's rows, which the next group overwrites).
     // Touch every 128-byte line of the next group's rows now, so that its
-    // tile load after this drain hits the caches.  (Loads in inline asm: the
-    // compiler neither drops them nor tracks them; its own waits can only
-    // over-wait because of them, and the drain's end waits for them.)
+    // tile load after this drain hits the caches.  Relaxed atomic loads: the
+    // compiler issues them here (it does not sink an atomic) and tracks
+    // their destination registers like any load (its vmcnt waits count
+    // them); the values are consumed only at the drain's end, so nothing
+    // waits for them before.  (an asm-issued load's register was
+    // invisible to the compiler.)
     uint32_t pfa = 0, pfb = 0;
     if (gnn < ngroups) {
       const unsigned long long sn = s_begin + gnn * GROUP;
       const int lines = ((int)min<unsigned long long>((unsigned long long)GROUP, s_end - sn) * W + 31) / 32;
       const uint32_t* pa = ring_row(cur, sn, W) + 32 * min(lane, lines - 1);
       const uint32_t* pb = ring_row(cur, sn, W) + 32 * min(lane + 64, lines - 1);
-      asm volatile("global_load_dword %0, %1, off" : "=v"(pfa) : "v"(pa) : "memory");
-      asm volatile("global_load_dword %0, %1, off" : "=v"(pfb) : "v"(pb) : "memory");
+      pfa = __hip_atomic_load(pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pfb = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     resolve();
     if (async_cas) {  // the CAS this resolve set up, then its result

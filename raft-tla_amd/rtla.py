@@ -101,6 +101,8 @@ def _load():
         "rtla_synthetic_dedup": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(_Stats)]),
         "rtla_orbit_key": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_uint64), P(C.c_int)]),
         "rtla_permute_row": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_int), P(C.c_uint32)]),
+        "rtla_rows_text_hash": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, C.c_int, P(C.c_uint64)]),
+        "rtla_level_text_hash": (C.c_int, [C.c_void_p, C.c_int, P(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -116,7 +118,8 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_expand_batch", "rtla_state_text", "rtla_action_name", "rtla_invariants", "rtla_row_fingerprint",
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
             "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step",
-            "rtla_synthetic_generate", "rtla_synthetic_dedup", "rtla_orbit_key", "rtla_permute_row"]
+            "rtla_synthetic_generate", "rtla_synthetic_dedup", "rtla_orbit_key", "rtla_permute_row",
+            "rtla_rows_text_hash", "rtla_level_text_hash"]
 
 SYNTH_SEED = 0x5AF72025  # the synthetic microbench's PRNG seed
 
@@ -253,6 +256,20 @@ def permute_row(cfg: Config, row: Sequence[int], pi: Sequence[int]):
     out = (C.c_uint32 * len(row))()
     _check(_lib.rtla_permute_row(C.byref(cc), arr, p, out), "rtla_permute_row")
     return list(out)
+
+
+def rows_text_hash(cfg: Config, rows: Sequence[Sequence[int]], threads: int = 0) -> int:
+    """Sum mod 2^64 of FNV-1a-64(state_text) over the rows: the oracle's
+    per-level digest of a set of states (host threads, rtla_rows_text_hash)."""
+    cc = cfg.c()
+    w = row_words(cfg)
+    n = len(rows)
+    flat = (C.c_uint32 * max(1, n * w))()
+    for k, r in enumerate(rows):
+        flat[k * w:(k + 1) * w] = list(r)
+    out = C.c_uint64(0)
+    _check(_lib.rtla_rows_text_hash(C.byref(cc), flat, n, threads, C.byref(out)), "rtla_rows_text_hash")
+    return out.value
 
 
 def stored_fingerprint(row: Sequence[int]):
@@ -396,6 +413,14 @@ class Checker:
         buf = (C.c_uint32 * max(1, n.value * w))()
         _check(_lib.rtla_frontier(self._h, buf, n.value, C.byref(n)), "rtla_frontier")
         return [list(buf[k * w:(k + 1) * w]) for k in range(n.value)]
+
+    def level_text_hash(self, threads: int = 0) -> int:
+        """Digest of the level last produced (all shards / ranks): sum mod 2^64
+        of FNV-1a-64 of each state's text, decoded on the host from the device
+        rows in chunks -- compared with the oracle's level_text_hash."""
+        out = C.c_uint64(0)
+        _check(_lib.rtla_level_text_hash(self._h, threads, C.byref(out)), "rtla_level_text_hash")
+        return out.value
 
     def checkpoint(self, prefix: str):
         """TLC -checkpoint: write the search to <prefix>.shard<id>.rtla (between levels)."""

@@ -43,17 +43,20 @@ SYM_CASES = {
     "n3_v1_t2_l1_m2_sym": (3, 1, 2, 1, 1, 2, (NTL,), False, True),
 }
 # Models too large for the CPU oracle to exhaust here: a bounded prefix of
-# complete BFS levels (the oracle stops after the first level that passes
-# max_distinct), with each level's state-text hash.
-# name: (N, V, T, L, C, M, invariants, max_distinct)
+# complete BFS levels, with each level's state-text hash.  The oracle stops
+# after the first level that passes max_distinct, or after max_levels levels
+# (its last level counted, hashed and deduplicated but not kept: one level
+# deeper in the same memory).  The BASELINE configs are pinned to the depth
+# bench.py times them at (the levels that fit one MI355X's HBM).
+# name: (N, V, T, L, C, M, invariants, max_distinct, max_levels)
 PREFIXES = {
     # bench.py's exhaust model (wall time to exhaust)
-    "n3_v2_t2_l2_m2_prefix": (3, 2, 2, 2, 1, 2, (ES, LM), 200_000_000),
+    "n3_v2_t2_l2_m2_prefix": (3, 2, 2, 2, 1, 2, (ES, LM), 200_000_000, 0),
     # BASELINE.json configs[1] and configs[0] exactly as stated (no in-flight bound)
-    "n3_v2_t3_l2_c1_prefix": (3, 2, 3, 2, 1, 0, (ES, LM), 25_000_000),
-    "n3_v1_t2_l1_c1_prefix": (3, 1, 2, 1, 1, 0, (NTL,), 30_000_000),
+    "n3_v2_t3_l2_c1_prefix": (3, 2, 3, 2, 1, 0, (ES, LM), 0, 17),
+    "n3_v1_t2_l1_c1_prefix": (3, 1, 2, 1, 1, 0, (NTL,), 0, 23),
     # BASELINE.json configs[2] as stated (2 copies per message: Duplicate/Drop live)
-    "n3_v2_t4_l3_c2_prefix": (3, 2, 4, 3, 2, 0, (), 20_000_000),
+    "n3_v2_t4_l3_c2_prefix": (3, 2, 4, 3, 2, 0, (), 0, 14),
 }
 # SYMMETRY prefixes (orbit counts per level; no text hashes: the orbit
 # representatives kept differ between implementations).  N = 4 and BASELINE
@@ -109,10 +112,11 @@ def main():
             case["source"] += " + oracle/raft_values.py (orbit key: least text over permutations)"
         out[name] = case
         print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
-    for name, (n, v, t, l, c, m, inv, cap) in PREFIXES.items():
+    for name, (n, v, t, l, c, m, inv, cap, depth) in PREFIXES.items():
         if not big or (only and name not in only):
             continue
-        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap)
+        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap, max_levels=depth)
+        cfg.verbose = 1
         r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, text_hash=True)
         assert r["rc"] in (0, -4), (name, r["rc"])
         out[name] = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
@@ -121,6 +125,8 @@ def main():
                      "level_text_hash": ["%016x" % h for h in r["level_text_hash"]],
                      "source": "oracle/raft_cpu.c, first %d complete levels" % len(r["levels"])}
         print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
+        with open(path, "w") as f:  # each prefix is long: keep what is done
+            json.dump(out, f, indent=1, sort_keys=True)
     for name, (n, v, t, l, c, m, inv, cap) in SYM_PREFIXES.items():
         if not big or (only and name not in only):
             continue

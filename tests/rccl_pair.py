@@ -34,6 +34,26 @@ def main():
                       tuple(g["invariants"]), fpset_log2=log2, mem_budget=(8 << log2) * 3 + (1 << 29),
                       symmetry=bool(g.get("symmetry", False)), chunk=int(os.environ.get("RCCL_PAIR_CHUNK", "0")))
     levels = []
+    if os.environ.get("RCCL_PAIR_MODE") == "recover_missing":
+        # checkpoint after 3 levels, the last rank loses its file, every rank
+        # recovers: all must fail, promptly (no rank left waiting)
+        prefix = sys.argv[5]
+        with rtla.Checker(cfg, rank=rank, world=world, comm_id=cid) as ck:
+            ck.init()
+            for _ in range(3):
+                ck.step()
+            ck.checkpoint(prefix)
+            if rank == world - 1:
+                os.remove("%s.shard%d.rtla" % (prefix, rank))
+            t0 = time.time()
+            try:
+                ck.recover(prefix)
+                out = {"rank": rank, "recover": 0}
+            except rtla.RtlaError as e:
+                out = {"rank": rank, "recover": e.status}
+            out["seconds"] = time.time() - t0
+        print(json.dumps(out), flush=True)
+        return
     with rtla.Checker(cfg, rank=rank, world=world, comm_id=cid) as ck:
         st = ck.init()
         while st == rtla.OK:

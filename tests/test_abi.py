@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 def test_python_mirror_binds_every_symbol():
     import rtla
     assert sorted(rtla.EXPORTED) == declared_symbols()
-    assert rtla._lib.rtla_abi_version() == 5
+    assert rtla._lib.rtla_abi_version() == 6
 
 
 def test_row_layout_and_config_errors():
@@ -70,3 +70,16 @@ def test_open_refuses_more_shards_than_the_outbox_holds():
         with pytest.raises(rtla.RtlaError) as e:
             rtla.Checker(rtla.Config(2, 1, 2, 1, 1, 1, **kw))
         assert e.value.status == -1
+
+
+def test_rows_text_hash_is_the_oracle_digest():
+    """rtla_rows_text_hash (host threads) = the sum of FNV-1a-64 of each row's
+    text, the digest the C oracle records per level (raft_cpu.text_hash)."""
+    import raft_cpu
+    import rtla
+    cfg = rtla.Config(3, 2, 4, 3, 2, 0, ("ElectionSafety",), bag_cap=12)
+    rows = rtla.random_rows(cfg, 0, 3000, pool=500)
+    want = sum(raft_cpu.text_hash(rtla.state_text(cfg, r)) for r in rows) & (2**64 - 1)
+    assert rtla.rows_text_hash(cfg, rows) == want
+    assert rtla.rows_text_hash(cfg, rows, threads=1) == want
+    assert rtla.rows_text_hash(cfg, []) == 0

@@ -168,7 +168,8 @@ PREFIX = sorted(k for k, v in GOLD.items() if v.get("prefix"))
 @pytest.mark.parametrize("name", BIG)
 def test_full_size_counts_match_golden(name):
     """The oracle's largest exhausted models (up to 1.45e8 states): every
-    level's counts, and the set of states of every level of <= 200k states."""
+    level's counts, and the set of states of every level (the level digest of
+    the decoded GPU rows, rtla_level_text_hash, against the oracle's)."""
     g = GOLD[name]
     cfg = cfg_of(g, fpset_log2=(g["distinct"] * 3).bit_length())
     hashes = g.get("level_text_hash", [])
@@ -176,8 +177,8 @@ def test_full_size_counts_match_golden(name):
         st = ck.init()
         while True:
             k = len(ck.levels) - 1
-            if k < len(hashes) and ck.levels[-1].new <= 200_000 and not g.get("symmetry"):
-                assert level_text_hash(cfg, ck.frontier()) == hashes[k], "level %d" % (k + 1)
+            if k < len(hashes) and not g.get("symmetry"):
+                assert "%016x" % ck.level_text_hash() == hashes[k], "level %d" % (k + 1)
             if st != rtla.OK:
                 break
             st = ck.step()
@@ -195,21 +196,34 @@ def level_text_hash(cfg, rows):
     return "%016x" % (sum(raft_cpu.text_hash(rtla.state_text(cfg, r)) for r in rows) & (2**64 - 1))
 
 
+def test_level_digest_equals_python_recount():
+    """rtla_level_text_hash (device rows streamed to host threads) equals the
+    digest recomputed row by row through rtla_state_text + the oracle's FNV."""
+    g = GOLD["n2_v2_t3_l2_m1"]
+    cfg = cfg_of(g, shards=2, chunk=512, **small_kw(g))
+    with rtla.Checker(cfg) as ck:
+        ck.init()
+        for _ in range(7):
+            ck.step()
+        assert "%016x" % ck.level_text_hash() == level_text_hash(cfg, ck.frontier()) == g["level_text_hash"][7]
+
+
 @pytest.mark.parametrize("name", PREFIX)
 def test_prefix_levels_match_golden(name):
-    """Models too large for the CPU oracle -- BASELINE configs[0] and [1]
-    exactly as stated, and bench.py's exhaust model: the first complete BFS
-    levels the oracle could afford must match exactly, counts at every level
-    and the set of states (text hash) at every level of <= 200k states."""
+    """Models too large for the CPU oracle to exhaust -- BASELINE configs[0],
+    [1] and [2] exactly as stated, to the depth bench.py times them at, the
+    exhaust model's first 31 levels, and the SYMMETRY prefixes: per-level
+    counts, and (non-symmetric) the set of states of EVERY level: the level
+    digest of the decoded GPU rows against the oracle's."""
     g = GOLD[name]
-    cfg = cfg_of(g, fpset_log2=30, bag_cap=PREFIX_BAG.get(name, 0))
+    cfg = cfg_of(g, fpset_log2=max(30, (g["distinct"] * 3).bit_length()), bag_cap=PREFIX_BAG.get(name, 0))
     hashes = g.get("level_text_hash", [])
     with rtla.Checker(cfg) as ck:
         st = ck.init()
         while True:
             k = len(ck.levels) - 1
-            if k < len(hashes) and ck.levels[-1].new <= 200_000:
-                assert level_text_hash(cfg, ck.frontier()) == hashes[k], "level %d" % (k + 1)
+            if k < len(hashes):
+                assert "%016x" % ck.level_text_hash() == hashes[k], "level %d" % (k + 1)
             if len(ck.levels) >= len(g["levels"]):
                 break
             assert st == rtla.OK
@@ -647,6 +661,26 @@ def test_ranks_over_shm_transport_match_golden(tmp_path, name, world):
         assert all(o["status"] == rtla.VIOLATION for o in outs)
         assert all(len(o["trace"]) == g["trace_len"] for o in outs)
         assert outs[0]["trace"] == outs[1]["trace"]
+
+
+def test_ranks_recover_fails_on_every_rank(tmp_path):
+    """One rank's checkpoint file is missing: rtla_recover fails on EVERY rank
+    and returns promptly -- the local failure travels in the cross-rank
+    consistency reduction instead of leaving the other ranks waiting in it."""
+    import subprocess
+    import sys
+    env = dict(os.environ, RTLA_TRANSPORT="shm", RTLA_SHM_SLOT_MB="32", RCCL_PAIR_MODE="recover_missing")
+    idfile, prefix = str(tmp_path / "comm_id"), str(tmp_path / "ckpt")
+    helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_pair.py")
+    procs = [subprocess.Popen([sys.executable, helper, str(r), "2", idfile, "n3_v1_t2_l1_m1", prefix], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=120)
+        assert p.returncode == 0, e[-2000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    assert [o["recover"] for o in outs] == [-5, -6]  # the other rank's failure / the missing file
+    assert all(o["seconds"] < 30 for o in outs)
 
 
 def test_synthetic_resident_dedup_matches_step():

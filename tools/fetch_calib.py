@@ -1,7 +1,7 @@
 """Calibrate rocprofv3 FETCH_SIZE / WRITE_SIZE on gfx950 for the two access
 shapes of the level kernel, by running kernels whose byte counts are known
 exactly (run under `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`, one
-pass each; tools/pmc_summary.py --calib divides the counters by these):
+pass each; tools/prof_summary.py divides the counters by these):
 
   1. k_probe_bench x3 (rtla_probe_bench2): n 8-byte accesses at uniformly
      random slots of a 2^30-slot table -- CAS inserts, CAS re-probes, load

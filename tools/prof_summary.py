@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_r02.sh run (gpurun_out/prof): per workload the
+"""Summarise a tools/profile.sh run (gpurun_out/prof): per workload the
 kernel-trace stats and PMC counters of k_expand_compact, HBM bytes per launch
 from FETCH_SIZE / WRITE_SIZE corrected by the calibration of
 tools/fetch_calib.py (known byte counts, same gfx950 counters), and a

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Profiling session (round 2): for each workload a kernel trace with stats and
+# Profiling session (round 2 onwards): for each workload a kernel trace with stats and
 # PMC passes (FETCH_SIZE and WRITE_SIZE in passes of their own, two SQ
 # groups), plus the FETCH/WRITE calibration of tools/fetch_calib.py.  Each GPU
 # step has its own time limit; any failure ends the script.
