@@ -77,6 +77,9 @@ enum {
   XF_WAVE_KERNEL = 2048,  // use the wave-per-state k_expand (the fallback for rows too wide for the compact tile)
   XF_NO_SPECIAL = 4096,   // compact kernel: run-time layout even for a compiled-in configuration
   XF_DEDUP_ONLY = 8192,   // compact kernel: count new fingerprints, build no rows (synthetic microbench)
+  XF_ALL_SUCCESSORS = 16384,  // compact kernel: no seen set -- every enabled successor (in-model or not) gets a
+                              // row, its record = input index << 32 | in_model << 31 | sub << 16 | instance
+                              // (rtla_expand_batch: the parity seam runs the hot kernel)
 };
 
 // Per-level device counters (zeroed before each level except `cover`).

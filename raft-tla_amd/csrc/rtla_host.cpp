@@ -534,18 +534,44 @@ static void report_flags(int flags) {
   if (flags & FLAG_BAD_INDEX) fprintf(stderr, "rtla: checked build: a kernel index left its buffer\n");
 }
 
-// Run k_expand_batch on device rows; results copied to host, sorted by (input, instance).
+// RTLA_XFLAGS: kernel-variant switches (XF_* in rtla_device.h) for performance
+// experiments; results are identical for the variants that do not skip work.
+static int env_xflags() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RTLA_XFLAGS");
+    v = e ? (atoi(e) & (XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL | XF_NO_SPECIAL)) : 0;
+  }
+  return v;
+}
+
+// Every enabled successor of n device rows (d_rows holds round64(n) rows),
+// copied to the host sorted by (input, instance).  The level kernel itself
+// runs it -- k_expand_compact with XF_ALL_SUCCESSORS: the same evaluation,
+// fingerprint derivation and row building as the BFS, minus the seen set --
+// so this parity seam checks the hot kernel; layouts too wide for its LDS
+// tile (and RTLA_XFLAGS=2048) use the wave-per-state k_expand_batch.
 static int expand_batch_dev(const Layout& L, const uint32_t* d_rows, size_t n, std::vector<uint32_t>& out,
                             std::vector<uint64_t>& info, hipStream_t st) {
-  size_t cap = n * (size_t)L.fam[F_COUNT];
+  size_t cap = round64(std::max<size_t>(n, 1) * (size_t)L.fam[F_COUNT]);
   uint32_t* d_out = nullptr;
   uint64_t* d_info = nullptr;
   DevCounters* d_ctr = nullptr;
-  HIPCHK(hipMalloc(&d_out, std::max<size_t>(cap, 1) * L.W * 4));
-  HIPCHK(hipMalloc(&d_info, std::max<size_t>(cap, 1) * 8));
+  HIPCHK(hipMalloc(&d_out, cap * L.W * 4));
+  HIPCHK(hipMalloc(&d_info, cap * 8));
   HIPCHK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   HIPCHK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), st));
-  HIPCHK(launch_expand_batch(L, d_rows, n, d_out, d_info, cap, d_ctr, st));
+  const bool hot = expand_compact_wpb(L) > 0 && !(env_xflags() & XF_WAVE_KERNEL);
+  if (hot) {
+    const uint64_t caps[3] = {round64(n), cap, cap};  // DevCounters cap_cur / cap_next / cap_parents
+    HIPCHK(hipMemcpyAsync(&d_ctr->cap_cur, caps, sizeof caps, hipMemcpyHostToDevice, st));
+    const Ring cur{const_cast<uint32_t*>(d_rows), 0, round64(n)}, next{d_out, 0, cap};
+    ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+    HIPCHK(launch_expand(L, cur, 0, n, 0, next, d_info, 0, cap, nullptr, 1, d_ctr, box, 0, st,
+                         XF_ALL_SUCCESSORS | XF_NO_COVER, nullptr));
+  } else {
+    HIPCHK(launch_expand_batch(L, d_rows, n, d_out, d_info, cap, d_ctr, st));
+  }
   DevCounters h;
   HIPCHK(hipMemcpyAsync(&h, d_ctr, sizeof h, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -585,7 +611,7 @@ extern "C" int rtla_expand_batch(const rtla_cfg* c, const uint32_t* rows, size_t
   if (r) return r;
   if (!rows || !n_out) return RTLA_E_ARG;
   uint32_t* d_rows = nullptr;
-  HIPCHK(hipMalloc(&d_rows, std::max<size_t>(n, 1) * L.W * 4));
+  HIPCHK(hipMalloc(&d_rows, round64(std::max<size_t>(n, 1)) * L.W * 4));
   HIPCHK(hipMemcpy(d_rows, rows, n * L.W * 4, hipMemcpyHostToDevice));
   std::vector<uint32_t> out;
   std::vector<uint64_t> inf;
@@ -796,17 +822,6 @@ extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
            p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
            (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk);
   return RTLA_OK;
-}
-
-// RTLA_XFLAGS: kernel-variant switches (XF_* in rtla_device.h) for performance
-// experiments; results are identical for the variants that do not skip work.
-static int env_xflags() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RTLA_XFLAGS");
-    v = e ? (atoi(e) & (XF_GENERIC_DELTA | XF_BLOCK4 | XF_NO_PERSIST | XF_CAS_ONLY | XF_WAVE_KERNEL | XF_NO_SPECIAL)) : 0;
-  }
-  return v;
 }
 
 static double now_s() {
@@ -1509,7 +1524,7 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
   if (n > cap) return RTLA_E_ARG;
   std::vector<uint32_t> row = x->init_row;
   uint32_t* d_row = nullptr;
-  HIPCHK(hipMalloc(&d_row, L.W * 4));
+  HIPCHK(hipMalloc(&d_row, 64 * L.W * 4));  // a whole 64-row group (the level kernel's tile)
   if (rows) memcpy(rows, row.data(), L.W * 4);
   if (labels) labels[0] = -1;
   int rc = RTLA_OK;

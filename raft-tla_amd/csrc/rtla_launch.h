@@ -16,6 +16,32 @@ int expand_compact_wpb(const Layout& L);
 // Blocks of 4 waves that fit on one CU given the LDS footprint.
 int expand_blocks_per_cu(const Layout& L);
 
+// Arguments of one level-kernel launch (k_expand_compact).
+struct CompactArgs {
+  Layout L;
+  bool multi;
+  Ring cur;
+  uint64_t s_begin, s_end, cur_base;
+  Ring next;
+  uint64_t* parents;
+  uint64_t next_base, next_cap;
+  uint64_t* table;
+  int tlog2;
+  DevCounters* ctr;
+  ShardBox box;
+  hipStream_t st;
+  int xflags;
+  uint64_t* sent;
+  int wpb;
+};
+// The level kernel's instantiations, one translation unit each (compiled in
+// parallel): *done = false if the unit has no kernel for a.L.
+hipError_t launch_compact_spec_a(const CompactArgs& a, bool* done);     // configs[1], configs[0], exhaust
+hipError_t launch_compact_spec_b(const CompactArgs& a, bool* done);     // configs[2], configs[4], configs[3] (SYMMETRY)
+hipError_t launch_compact_sym(const CompactArgs& a, bool* done);        // SYMMETRY, run-time layout
+hipError_t launch_compact_generic_a(const CompactArgs& a, bool* done);  // N = 1..3, run-time layout
+hipError_t launch_compact_generic_b(const CompactArgs& a, bool* done);  // N = 4, 5, run-time layout
+
 hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uint64_t s_end,
                          uint64_t cur_base, const Ring& next, uint64_t* parents, uint64_t next_base,
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Build a perf-experiment variant of librtla.so into exp/<name>/ (extra -D flags).
+# Build a perf-experiment variant of librtla.so into exp/<name>/ (extra -D flags),
+# all translation units in parallel.
 set -e
 name=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -7,9 +8,11 @@ D=$ROOT/exp/$name; mkdir -p $D
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
 S=$ROOT/raft-tla_amd/csrc
-$H $F -c -o $D/k.o $S/rtla_kernels.hip &
+for u in rtla_kernels rtla_kspec_a rtla_kspec_b rtla_ksym rtla_kgeneric_a rtla_kgeneric_b; do
+  $H $F -c -o $D/$u.o $S/$u.hip &
+done
 $H $F -c -o $D/h.o $S/rtla_host.cpp &
 $H $F -c -o $D/t.o $S/rtla_text.cpp &
 wait
-$H -shared -fPIC --offload-arch=gfx950 -o $D/librtla.so $D/k.o $D/h.o $D/t.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$H -shared -fPIC --offload-arch=gfx950 -o $D/librtla.so $D/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f $D/*.o
