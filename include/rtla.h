@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 6
+#define RTLA_ABI_VERSION 7
 
 /* status codes */
 #define RTLA_OK 0
@@ -145,6 +145,10 @@ int rtla_device_info(rtla_ctx *ctx, char *buf, size_t cap);
 
 /* Stateless helpers (need a GPU only for rtla_expand_batch). */
 int rtla_row_words(const rtla_cfg *cfg);
+/* Geometry of the packed row (u32 words; raft-tla_amd/csrc/rtla_model.h):
+ * out[0..10) = W, off_hdr, off_srv, srv_words, off_all, all_words, off_elec,
+ * elec_words, off_bag, slot_words.  Returns the number of values written. */
+int rtla_row_layout(const rtla_cfg *cfg, int32_t *out, int n);
 int rtla_init_row(const rtla_cfg *cfg, uint32_t *row);
 /* Every enabled successor of each input row.  succ: cap rows; info[k] =
  * input index << 32 | in_model << 31 | receive-sub << 16 | instance. */

@@ -362,6 +362,18 @@ extern "C" int rtla_row_words(const rtla_cfg* c) {
   return r ? r : L.W;
 }
 
+extern "C" int rtla_row_layout(const rtla_cfg* c, int32_t* out, int n) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  if (!out) return RTLA_E_ARG;
+  const int32_t v[10] = {L.W, L.off_hdr, L.off_srv, L.srv_w, L.off_all, L.all_words, L.off_elec, L.elec_w, L.off_bag,
+                         L.slot_w};
+  const int m = std::min(n, 10);
+  for (int k = 0; k < m; k++) out[k] = v[k];
+  return m;
+}
+
 extern "C" int rtla_init_row(const rtla_cfg* c, uint32_t* row) {
   Layout L;
   int r = layout_from_cfg(c, &L);

@@ -239,7 +239,7 @@ __device__ __forceinline__ FP successor_orbit_key(const Layout& L, P prow, const
   constexpr int EW = 2 + NS;
   const int ne0 = row_nelec(L, prow);
   return sym_key<NS>(
-      [&](int i, uint32_t* out) {
+      L, [&](int i, uint32_t* out) {
         load_rec<NS>(L, prow, i, out);
         if (i == d.srv) {
 #pragma unroll
@@ -249,8 +249,10 @@ __device__ __forceinline__ FP successor_orbit_key(const Layout& L, P prow, const
       d.nmsg, [&](int q) { return bag_get(L, prow, d, q); }, ne0 + (d.elec ? 1 : 0),
       [&](int e, uint32_t* out) {
         if (e < ne0) {
+          out[0] = elec_w0(L, prow, e);
+          out[1] = elec_log(L, prow, e);
 #pragma unroll
-          for (int w = 0; w < EW; w++) out[w] = prow[L.off_elec + e * EW + w];
+          for (int j = 0; j < NS; j++) out[2 + j] = elec_vl(L, prow, e, j);
         } else {
 #pragma unroll
           for (int w = 0; w < EW; w++) out[w] = d.erec[w];
@@ -325,7 +327,12 @@ __host__ __device__ constexpr int lane_lds_words(int W, int AW) { return 64 * W 
 namespace {
 
 constexpr int RING = 128;   // pair ring (u16: state lane << 8 | instance - window base)
-constexpr int NEWCAP = 256; // new-state list (u16: state lane << 8 | instance)
+constexpr int NEWCAP = 512; // new-state list (u16: state lane << 8 | instance)
+// The list is built into rows at the group's end; a group that finds more
+// new states (early levels) flushes it when it holds more than this many --
+// after which one chunk (<= 64) and a drain (<= 2 x 64) may still add
+// entries before the flush.
+constexpr int NEWFLUSH = NEWCAP - 3 * 64;
 
 constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
 
@@ -352,11 +359,10 @@ __device__ __forceinline__ unsigned long long win_bits(unsigned long long bits, 
 template <int NS>
 __device__ __forceinline__ unsigned long long cand_mask(const Layout& L, const uint32_t* row, int nmsg, int wb) {
   constexpr int N = NS;
-  const int SW = 3 + N;
   unsigned long long rv = 0, bl = 0, ldr = 0, tmo = 0;
 #pragma unroll
   for (int i = 0; i < N; i++) {
-    const uint32_t w0 = row[L.off_srv + i * SW];
+    const uint32_t w0 = srv_w0(L, row, i);
     const uint32_t role = s_role(w0);
     if (role == FOLLOWER || role == CANDIDATE) tmo |= 1ull << i;          // Timeout :178-181
     if (role == CANDIDATE) {
@@ -507,56 +513,46 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   uint32_t cinfo = 0;
   // New states found so far whose rows are not built yet: newl[head, tail)
   // (mod NEWCAP) holds (state lane, instance); their parents are rows of the
-  // current group (uniform counters).  A reservation of next-level slots for
-  // the oldest 64 is requested one chunk before they are built (res_ob: the
-  // atomic's result in lane 0, read only then).
+  // current group (uniform counters).  They are built when the group's probes
+  // have drained (build_all), so no probe or CAS state is live while the
+  // rows are built.
   int head = 0, tail = 0;
-  bool have_res = false;
-  unsigned long long res_ob = 0;
   unsigned long long dedup_new = 0;  // XF_DEDUP_ONLY: new fingerprints (uniform)
   unsigned long long s0 = 0;  // first state of the current group
 
-  // One atomic reserves nb next-level slots.  Slots past next_cap are
-  // dropped and flagged (the level is then reported incomplete).
-  auto reserve_issue = [&](int nb) {  // the atomic, not waited for
-    unsigned long long ob = 0;
-    if (lane == 0) ob = atomicAdd(&ctr->next_count, (unsigned long long)nb);
-    return ob;
-  };
-  auto reserve_take = [&](unsigned long long ob, int nb) {
-    ob = shfl0_u64(ob);
-    if (ob + nb > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
-    return ob;
-  };
-  // Build the rows of the nb oldest pending new states into slots obase ..
-  // obase + nb - 1 of the next level, one state per lane:
+  // Build the rows of every pending new state (probes drained), one
+  // next-level slot reservation for all of them (slots past next_cap are
+  // dropped and flagged: the level is then reported incomplete):
   //  (1) the wave copies each parent row (LDS) to its child's slot with
-  //      coalesced stores;
-  //  (2) each lane re-derives its successor's full Delta (compute_delta with
-  //      slot bookkeeping; the probe pass only folded it into a hash), its
-  //      fingerprint, invariants and distinct coverage -- arithmetic that
-  //      overlaps the stores and the chunk's probe loads in flight;
-  //  (3) after the stores completed, each lane stores the words in which its
-  //      child differs from the parent (child_patches, rtla_model.h).
-  // This replaces a separate row-building kernel: no parent-record read, no
-  // parent-row gather, no second launch.
-  auto build_rows = [&](unsigned long long obase, int nb) {
-    const bool act = lane < nb;
-    const int e = act ? newl[(head + lane) & (NEWCAP - 1)] : 0;
-    const int sl = e >> 8, inst = e & 255;
-    const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nb, next_cap - obase);
+  //      coalesced stores, for all of them;
+  //  (2) per batch of 64, one state per lane: its full Delta (compute_delta
+  //      with slot bookkeeping; the probe pass only folded it into a hash),
+  //      fingerprint, invariants and distinct coverage -- the first batch's
+  //      arithmetic overlaps the copies in flight;
+  //  (3) after the copies landed (one wait), each lane stores the words in
+  //      which its child differs from the parent (child_write, rtla_model.h).
+  // No separate row-building kernel: no parent-record read, no parent-row
+  // gather, no second launch.
+  auto build_all = [&]() {
+    const int ntot = tail - head;  // uniform
+    if (ntot == 0) return;
+    unsigned long long obase = 0;
+    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)ntot);
+    obase = shfl0_u64(obase);
+    if (obase + ntot > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)ntot, next_cap - obase);
     const bool rows_on = !(xflags & XF_NO_MATERIALIZE) && RTLA_IDX_OK(ctr, obase + nrows, ctr->cap_next + 1);
     const unsigned long long p0 = ring_idx(next, obase);
     const int n1 = (int)min<unsigned long long>(next.cap - p0, (unsigned long long)nrows) * W;  // words before the wrap
     uint32_t* d1 = next.base + p0 * (unsigned long long)W;
-    if (rows_on) {  // (1)
+    if (rows_on) {  // (1): word i of the run of nrows child rows, lane-contiguous
       const int nwords = nrows * W;
       int r = 0, w = lane;
       while (w >= W) { w -= W; r++; }
       for (int i0 = 0; i0 < nwords; i0 += 64) {
-        const int sr = __shfl(sl, r & 63);
         const int i = i0 + lane;
         if (i < nwords) {
+          const int sr = newl[(head + r) & (NEWCAP - 1)] >> 8;
           const uint32_t v = rows[sr * W + w];
           if (i < n1) d1[i] = v;
           else next.base[i - n1] = v;
@@ -565,53 +561,61 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         while (w >= W) { w -= W; r++; }
       }
     }
-    DeltaT<NS> d;  // (2)
-    d.enabled = 0;
-    if (act) compute_delta<NS>(L, rows + sl * W, inst, d);
-    const FP qfp = pfpl[sl];
-    FP cfp{0, 0};
-    int bad = 0;
-    if (act) {
-      const uint32_t* prow = rows + sl * W;
-      cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
-      bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-    }
-    if (!(xflags & XF_ALL_SUCCESSORS) && claim_violation(ctr, bad, lane)) {
-      ctr->viol_parent = cur_base + s0 + sl;
-      ctr->viol_inst = inst;
-      ctr->viol_in_model = 1;
-      ctr->viol_child = lane < nrows ? next_base + obase + lane : ~0ull;
-    }
-    if (!(xflags & XF_NO_COVER)) {  // distinct coverage, aggregated over equal codes
-      const int code = act ? cover_code(L, inst, d.sub) : -1;
-      const unsigned long long am = __ballot(act);
-      if (am) {
-        const int c0 = __shfl(code, __builtin_ctzll(am));
-        const bool same = act && code == c0;
-        const int n0 = __popcll(__ballot(same));
-        if (lane == 0) atomicAdd(&cov[COVER_CODES + c0], (unsigned)n0);
-        if (act && !same) atomicAdd(&cov[COVER_CODES + code], 1u);
+    for (int b = 0; b < ntot; b += 64) {  // (2), (3)
+      const bool act = b + lane < ntot;
+      const int e = act ? newl[(head + b + lane) & (NEWCAP - 1)] : 0;
+      const int sl = e >> 8, inst = e & 255;
+      const int child = b + lane;  // index in the run
+      DeltaT<NS> d;
+      d.enabled = 0;
+      if (act) compute_delta<NS>(L, rows + sl * W, inst, d);
+      const FP qfp = pfpl[sl];
+      FP cfp{0, 0};
+      int bad = 0;
+      if (act) {
+        const uint32_t* prow = rows + sl * W;
+        cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
+        bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
       }
-    }
-    if (rows_on) {  // (3): the copies must land first (same words, other lanes)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane < nrows) {
-        const StridedWords<GROUP> pall_p{pall + sl};
-        const int off = lane * W;
-        child_patches<NS>(L, rows + sl * W, d, pall_p, cfp, [&](int w, uint32_t v) {
-          const int i = off + w;
-          if (i < n1) d1[i] = v;
-          else next.base[i - n1] = v;
-        });
+      if (!(xflags & XF_ALL_SUCCESSORS) && claim_violation(ctr, bad, lane)) {
+        ctr->viol_parent = cur_base + s0 + sl;
+        ctr->viol_inst = inst;
+        ctr->viol_in_model = 1;
+        ctr->viol_child = child < nrows ? next_base + obase + child : ~0ull;
       }
+      if (!(xflags & XF_NO_COVER)) {  // distinct coverage, aggregated over equal codes
+        const int code = act ? cover_code(L, inst, d.sub) : -1;
+        const unsigned long long am = __ballot(act);
+        if (am) {
+          const int c0 = __shfl(code, __builtin_ctzll(am));
+          const bool same = act && code == c0;
+          const int n0 = __popcll(__ballot(same));
+          if (lane == 0) atomicAdd(&cov[COVER_CODES + c0], (unsigned)n0);
+          if (act && !same) atomicAdd(&cov[COVER_CODES + code], 1u);
+        }
+      }
+      uint32_t spk[PACKW], epk[PACKW];  // the changed records, packed
+      if (act) child_pack(L, d, spk, epk);
+      if (rows_on) {  // (3): the copies must land first (same words, other lanes)
+        if (b == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (child < nrows) {
+          const StridedWords<GROUP> pall_p{pall + sl};
+          const int off = child * W;
+          child_write(L, rows + sl * W, d, spk, epk, pall_p, cfp, [&](int w, uint32_t v) {
+            const int i = off + w;
+            if (i < n1) d1[i] = v;
+            else next.base[i - n1] = v;
+          });
+        }
+      }
+      if (child < nrows && RTLA_IDX_OK(ctr, next_base + obase + child, ctr->cap_parents))
+        parents[next_base + obase + child] =
+            (xflags & XF_ALL_SUCCESSORS)
+                ? (cur_base + s0 + sl) << 32 | (unsigned long long)(d.in_model ? 1u : 0u) << 31 |
+                      (unsigned long long)d.sub << 16 | (unsigned long long)inst
+                : (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
     }
-    if (lane < nrows && RTLA_IDX_OK(ctr, next_base + obase + lane, ctr->cap_parents))
-      parents[next_base + obase + lane] =
-          (xflags & XF_ALL_SUCCESSORS)
-              ? (cur_base + s0 + sl) << 32 | (unsigned long long)(d.in_model ? 1u : 0u) << 31 |
-                    (unsigned long long)d.sub << 16 | (unsigned long long)inst
-              : (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
-    head += nb;
+    head = tail;
   };
   auto issue_cas = [&]() {
     if (cpend) cold = atomicCAS(&table[cidx], 0ull, ckey);
@@ -803,13 +807,21 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     }
     nprobe = false;
   };
+  // Every probe in flight resolved: the last loads, then the CAS they set up.
+  auto drain = [&]() {
+    resolve();
+    if (async_cas) {
+      issue_cas();
+      resolve();
+    }
+  };
   // Append the pairs of instance q (bit q of this window's wave-wide mask)
   // to the ring, Receive grouped by message type (one handler of
   // raft.tla:421-436 per run).
   auto append_instance = [&](int& pos, unsigned long long mask, int wb, int q, const uint32_t* prow_mine, int f) {
     const bool mine = (mask >> q) & 1ull;
     if (f == F_RECEIVE) {
-      const uint32_t ty = mine ? m_type(bag_slot(L, prow_mine, wb + q - L.fam[F_RECEIVE])) : 0u;
+      const uint32_t ty = mine ? slot_type(L, prow_mine, wb + q - L.fam[F_RECEIVE]) : 0u;
 #pragma unroll
       for (uint32_t t = 0; t < 4; t++) {
         const bool b = mine && ty == t;
@@ -880,21 +892,13 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         STAMP(2);  // successor deltas, fingerprints, coverage, out-of-model invariants
         resolve();  // the previous chunk's probes, after this chunk's arithmetic
         STAMP(3);
-        // Rows of the oldest 64 pending new states, into the slots reserved
-        // one chunk ago -- before this chunk's probes are issued, so the
-        // row stores' completion wait (build_rows step 3) never waits for
-        // them.  Then reserve for the next 64 if they are pending already.
-        if (have_res) {
-          build_rows(reserve_take(res_ob, 64), 64);
-          have_res = false;
-        }
-        STAMP(5);
-        if (tail - head >= 64) {
-          res_ob = reserve_issue(64);
-          have_res = true;
-        }
         issue_probe();
-        STAMP(4);  // slot reservation, probe issue
+        STAMP(4);  // probe issue
+        if (tail - head > NEWFLUSH) {  // rare (early levels): drain the probes, build the rows so far
+          drain();
+          build_all();
+          STAMP(5);
+        }
         done += cnt;
       }
     }
@@ -916,19 +920,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       pfa = __hip_atomic_load(pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pfb = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    resolve();
-    if (async_cas) {  // the CAS this resolve set up, then its result
-      issue_cas();
-      resolve();
-    }
-    if (have_res) {
-      build_rows(reserve_take(res_ob, 64), 64);
-      have_res = false;
-    }
-    while (tail > head) {
-      const int nb = min(64, tail - head);
-      build_rows(reserve_take(reserve_issue(nb), nb), nb);
-    }
+    drain();
+    build_all();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("" ::"v"(pfa), "v"(pfb));
     wave_sync();
@@ -955,6 +948,19 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 }
 
 namespace rtla {
+
+#define RTLA_DISPATCH_N(L, KERNEL, ...)                        \
+  switch ((L).N) {                                             \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
+  }
+
+static inline unsigned grid_x(uint64_t n, int per_block) {
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + per_block - 1) / per_block, 4096));
+}
 
 // States per wave-group of k_expand_compact: 64, or 32 when 64 rows would
 // make the per-wave LDS tile so large that fewer than ~11 waves fit a CU.

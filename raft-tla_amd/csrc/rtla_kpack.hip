@@ -1,0 +1,186 @@
+// rtla_kpack.hip -- lane-per-state row builders: the multi-shard sender's
+// k_pack_rows and the wave-per-state k_expand_batch (the parity seam's
+// fallback for rows too wide for the level kernel).
+#include "rtla_kernels_common.h"
+
+// Sender side: materialise the queued successors whose owner answered "new"
+// with a rank in [lo, hi) into the owner's row region (row + parent record,
+// RW = W + 2 words per slot).  Invariants are checked here, where parent and
+// action are known; a violation is recorded against the local parent.
+template <int NS>
+__global__ void __launch_bounds__(256)
+k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
+            const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
+            const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap, unsigned long long lo,
+            unsigned long long hi, uint32_t* __restrict__ rows, unsigned long long rows_cap, DevCounters* ctr) {
+  // A wave scans 64 records of owner p (grid.y), compacts the winners of
+  // this sub-round, gathers their parent rows into LDS (one coalesced read
+  // per row), builds each successor in place and ships row + parent record
+  // to the slot the owner's answer names (one coalesced write per row).
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ unsigned int cov[COVER_CODES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int W = L.W, AW = L.all_words, RW = W + 2;
+  uint32_t* lrows = lds + wave * lane_lds_words(W, AW);
+  const LaneWords pall{lrows + 64 * W + lane};
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
+  __syncthreads();
+  const unsigned long long p = blockIdx.y;  // owner shard
+  const unsigned long long n = counts[p];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; k0 < n;
+       k0 += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const unsigned long long k = k0 + lane;
+    const unsigned long long i = p * cap + k;
+    const unsigned long long a = k < n ? ans[i] : 0ull;
+    const bool win = a != 0 && a - 1 >= lo && a - 1 < hi;
+    const unsigned long long m = __ballot(win);
+    if (!m) continue;
+    const int nw = __popcll(m);
+    // compact: winner number r of this wave = lane w_r
+    int r_of_lane = __popcll(m & below);
+    unsigned long long ref = win ? send_ref[i] : 0ull;
+    unsigned long long dslot = win ? a - 1 - lo : 0ull;
+    // lane r takes the r-th winner's (ref, dslot)
+    int src_lane = 0;
+    {
+      unsigned long long mm = m;
+      for (int r = 0; r < nw; r++) {
+        const int l = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        if (lane == r) src_lane = l;
+      }
+    }
+    (void)r_of_lane;
+    ref = shfl_u64(ref, src_lane);
+    dslot = shfl_u64(dslot, src_lane);
+    const bool act = lane < nw;
+    const unsigned long long s = ref >> 16;
+    const int inst = (int)(ref & 0xffffull);
+    gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
+    wave_sync();
+    uint32_t* prow = lrows + lane * W;
+    if (act) {
+      const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
+      DeltaT<NS> d;
+      compute_delta<NS>(L, prow, inst, d);
+      const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
+      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+      if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+        ctr->viol_parent = cur_base + s;
+        ctr->viol_inst = inst;
+        ctr->viol_in_model = 1;
+        ctr->viol_child = ~0ull;
+      }
+      atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
+      materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
+    }
+    wave_sync();
+    for (int r = 0; r < nw; r++) {
+      const unsigned long long ds = readlane_u64(dslot, r);
+      uint32_t* dst = rows + (p * rows_cap + ds) * (unsigned long long)RW;
+      for (int w = lane; w < W; w += 64) dst[w] = lrows[r * W + w];
+      if (lane == 0) {
+        const unsigned long long pr =
+            (unsigned long long)me << 56 | (cur_base + readlane_u64(s, r)) << 16 | (unsigned long long)__builtin_amdgcn_readlane(inst, r);
+        dst[W] = (uint32_t)pr;
+        dst[W + 1] = (uint32_t)(pr >> 32);
+      }
+    }
+    wave_sync();
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
+    if (cov[k]) atomicAdd(&ctr->cover[COVER_CODES + k], (unsigned long long)cov[k]);
+}
+
+// Parity seam: every enabled successor of every input row (in-model or not),
+// materialised.  out_info[k] = input index << 32 | in_model << 31 | sub << 16 | inst.
+template <int NS>
+__global__ void __launch_bounds__(256)
+k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n, uint32_t* __restrict__ out,
+               unsigned long long* __restrict__ out_info, unsigned long long cap, DevCounters* ctr) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int W = L.W;
+  uint32_t* prow = lds + wave * wave_lds_words(W);
+  uint32_t* pall = prow + even_words(W);
+  FP* hsrv = reinterpret_cast<FP*>(pall + 32);
+  uint32_t* stage = pall + 32 + 4 * NMAX;
+  const int fixed = L.fam[F_RECEIVE];
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wave; s < n;
+       s += (unsigned long long)gridDim.x * wpb) {
+    const FP pfp = load_parent<NS>(L, rows + s * (unsigned long long)W, prow, pall, hsrv, lane);
+    const int nmsg = row_nmsg(L, prow);
+    const int ncand = fixed + 3 * nmsg;
+    for (int base = 0; base < ncand; base += 64) {
+      const int q = base + lane;
+      DeltaT<NS> d;
+      d.enabled = 0;
+      int inst = 0;
+      if (q < ncand) {
+        inst = candidate_inst(L, q, nmsg);
+        compute_delta<NS>(L, prow, inst, d);
+      }
+      bool en = d.enabled != 0;
+      if (en && d.err) {
+        set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
+        en = false;
+      }
+      const unsigned long long m = __ballot(en);
+      const int cnt = __popcll(m);
+      if (!cnt) continue;
+      const int rank = __popcll(m & ((1ull << lane) - 1ull));
+      unsigned long long obase = 0;
+      if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)cnt);
+      obase = shfl0_u64(obase);
+      if (obase + cnt > cap) {
+        if (lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+        continue;
+      }
+      const FP cfp = en ? fp_add(pfp, delta_fp<NS>(L, prow, d)) : FP{0, 0};
+      for (int b = 0; b < cnt; b += STAGE_ROWS) {
+        if (en && rank >= b && rank < b + STAGE_ROWS) materialize<NS>(L, prow, d, pall, cfp, stage + (rank - b) * W);
+        wave_sync();
+        const int nb = min(STAGE_ROWS, cnt - b);
+        uint32_t* dst = out + (obase + b) * (unsigned long long)W;
+        for (int w = lane; w < nb * W; w += 64) dst[w] = stage[w];
+        wave_sync();
+      }
+      if (en)
+        out_info[obase + rank] = s << 32 | (unsigned long long)(d.in_model ? 1u : 0u) << 31 |
+                                 (unsigned long long)d.sub << 16 | (unsigned long long)inst;
+    }
+  }
+}
+
+namespace rtla {
+
+hipError_t launch_pack_rows(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+                            const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
+                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, uint64_t max_count,
+                            hipStream_t st) {
+  if (!max_count) return hipSuccess;
+  const int wpb = std::max(1, expand_lane_wpb(L));
+  const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+  RTLA_DISPATCH_N(L, k_pack_rows, dim3(grid_x(max_count, 64 * wpb), nshard), dim3(64 * wpb), lds, st, L, cur,
+                  (unsigned long long)cur_base, me, (const unsigned long long*)send_ref, ans,
+                  (const unsigned long long*)counts, nshard, (unsigned long long)cap, (unsigned long long)lo,
+                  (unsigned long long)hi, rows, (unsigned long long)rows_cap, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out, uint64_t* info,
+                               uint64_t cap, DevCounters* ctr, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + 3) / 4;
+  int grid = (int)(blocks < 4096 ? blocks : 4096);
+  RTLA_DISPATCH_N(L, k_expand_batch, dim3(grid), dim3(256), expand_lds_bytes(L, 4), st, L, rows,
+                  (unsigned long long)n, out, (unsigned long long*)info, (unsigned long long)cap, ctr);
+  return hipGetLastError();
+}
+
+}  // namespace rtla

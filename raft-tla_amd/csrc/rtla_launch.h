@@ -38,7 +38,8 @@ struct CompactArgs {
 // parallel): *done = false if the unit has no kernel for a.L.
 hipError_t launch_compact_spec_a(const CompactArgs& a, bool* done);     // configs[1], configs[0], exhaust
 hipError_t launch_compact_spec_b(const CompactArgs& a, bool* done);     // configs[2], configs[4], configs[3] (SYMMETRY)
-hipError_t launch_compact_sym(const CompactArgs& a, bool* done);        // SYMMETRY, run-time layout
+hipError_t launch_compact_sym_a(const CompactArgs& a, bool* done);      // SYMMETRY, N = 1..3, run-time layout
+hipError_t launch_compact_sym_b(const CompactArgs& a, bool* done);      // SYMMETRY, N = 4, 5, run-time layout
 hipError_t launch_compact_generic_a(const CompactArgs& a, bool* done);  // N = 1..3, run-time layout
 hipError_t launch_compact_generic_b(const CompactArgs& a, bool* done);  // N = 4, 5, run-time layout
 
@@ -47,6 +48,11 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
                          uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box,
                          int grid, hipStream_t st, int xflags = 0, uint64_t* sent = nullptr,
                          hipEvent_t mid = nullptr);  // recorded after the level kernel
+// The wave-per-state level kernel (rtla_kwave.hip).
+hipError_t launch_wave_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uint64_t s_end, uint64_t cur_base,
+                              const Ring& next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                              uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box, int grid,
+                              hipStream_t st);
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
                                 uint64_t max_count, hipStream_t st);

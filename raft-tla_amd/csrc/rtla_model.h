@@ -10,31 +10,48 @@
 // below cites the lines it follows.
 //
 // ---------------------------------------------------------------------------
-// Row layout (u32 words; all offsets from rtla::Layout):
-//   [0..4)            fingerprint (a.lo, a.hi, b.lo, b.hi) of this state
-//   [off_hdr]         nmsg (bits 0-7) | nelec (bits 8-15)
-//   [off_srv + i*SW]  server record i, SW = 3 + N words:
+// Two formats.
+//
+// WIDE (in registers; what the actions compute on): a server record is 3 + N
+// u32 words
 //       w0 scalars:   currentTerm 0-3 | state 4-5 | votedFor 6-8 (7 = Nil)
 //                     | commitIndex 9-11 | votesResponded 12-16
 //                     | votesGranted 17-21 | DOMAIN voterLog[i] 22-26
 //       w1 log[i]     (log code, below)
 //       w2            nextIndex[i][j] at 3j | matchIndex[i][j] at 15+3j
 //       w3+j          voterLog[i][j] (log code; 0 unless bit j of the domain)
-//   [off_all]         allLogs: bitmask over the in-model log universe
-//   [off_elec + e*EW] elections, EW = 2 + N words, nelec records:
+// an election record 2 + N words
 //       w0 eterm 0-3 | eleader 4-6 | evotes 7-11 | DOMAIN evoterLog 12-16
 //       w1 elog, w2+j evoterLog[j]
-//   [off_bag + 2k]    message bag slot k (u64: key | count << 60), nmsg used
-//
-// Log code (u32): length in bits 0-2; entry k (0-based) at bits 3+5k:
-//   term (3 bits) | value << 3 (2 bits).
-// Message key (u64), fields by type (raft.tla:193-198, :215-225, :294-301, :338-343):
+// a message a u64 (key | count << 60).  Log code (u32): length in bits 0-2;
+// entry k (0-based) at bits 3+5k: term (3 bits) | value << 3 (2 bits).
+// Message key, fields by type (raft.tla:193-198, :215-225, :294-301, :338-343):
 //   type 0-1 | msource 2-4 | mdest 5-7 | mterm 8-11 |
 //   RVReq:  mlastLogTerm 12-15 | mlastLogIndex 16-18
 //   RVResp: mvoteGranted 12 | mlog 16-43
 //   AEReq:  mprevLogIndex 12-14 | mprevLogTerm 15-18 | has-entry 19 |
 //           entry 20-24 | mcommitIndex 25-27 | mlog 28-55
 //   AEResp: msuccess 12 | mmatchIndex 13-15
+//
+// ROW (HBM, LDS, the ABI; u32 words, offsets from rtla::Layout): the same
+// values bit-packed with the model's own field widths (make_layout), every
+// record starting on a word boundary:
+//   [0..4)                   fingerprint (a.lo, a.hi, b.lo, b.hi) of this state
+//   [off_hdr]                nmsg (bits 0-7) | nelec (bits 8-15)
+//   [off_srv + i*srv_w]      server i: currentTerm-1 | state | votedFor (N = Nil)
+//                            | commitIndex | votesResponded | votesGranted
+//                            | DOMAIN voterLog | log | per j: nextIndex-1,
+//                            matchIndex | per j: voterLog[i][j]
+//   [off_all]                allLogs: bitmask over the in-model log universe
+//   [off_elec + e*elec_w]    election e: eterm-1 | eleader | evotes | DOMAIN
+//                            evoterLog | elog | per j: evoterLog[j]
+//   [off_bag + k*slot_w]     bag slot k (0 = empty): type | msource | mdest |
+//                            mterm-1 | the type's fields | count
+// A packed log is length | entries (term-1 | value); a server's own log has
+// room for L+1 entries and its term for T+1 (the out-of-model successors of
+// ClientRequest / AppendEntries and of Timeout, which the parity seam
+// returns); every other log, term and index is bounded by the model (it was
+// written by an in-model state).  configs[1]: 172-byte rows (372 wide).
 //
 // The bag, the elections list and the bag slots are NOT kept in canonical
 // order.  State identity is decided only by the fingerprint, which is a sum
@@ -64,7 +81,7 @@ constexpr int VMAX = 4;   // values
 constexpr int CMAX = 14;  // MaxCopies (rows hold MaxCopies+1)
 constexpr int KMAX = 64;  // bag slots
 constexpr int EMAX = 32;  // election records
-constexpr int WMAX = 4 + 1 + NMAX * (3 + NMAX) + 32 + EMAX * (2 + NMAX) + 2 * KMAX;
+constexpr int WMAX = 4 + 1 + NMAX * 6 + 32 + EMAX * 6 + 2 * KMAX;  // widest row (words)
 
 enum { FOLLOWER = 0, CANDIDATE = 1, LEADER = 2 };
 enum { RVREQ = 0, RVRESP = 1, AEREQ = 2, AERESP = 3 };
@@ -93,12 +110,34 @@ struct Layout {
   int N, V, T, L, C, M, K, E;
   int inv_mask;
   int sym;             // SYMMETRY Permutations(Server): dedup by orbit key (orbit_key)
-  int SW, EW;
+  int SW, EW;          // WIDE record words: server 3 + N, election 2 + N
   int off_hdr, off_srv, off_all, all_words, off_elec, off_bag, W;
   int n_logs;          // |{logs of length <= L, terms 1..T}|
   int fam[F_COUNT + 1];  // first instance id of each family; fam[F_COUNT] = #instances
   int log_off[LMAX + 2];  // allLogs index offset of logs of length n
+  // ROW packing: field widths in bits
+  int b_tcur;  // currentTerm - 1        (0..T: Timeout's out-of-model successor reaches T+1)
+  int b_tm1;   // other terms - 1        (message, entry, election terms: 1..T)
+  int b_t0;    // terms 0..T             (mlastLogTerm, mprevLogTerm)
+  int b_vote;  // votedFor               (0..N-1, N = Nil)
+  int b_sid;   // a server id            (0..N-1)
+  int b_idx;   // an index 0..L          (commitIndex, nextIndex-1, matchIndex, message indexes)
+  int b_val;   // a value                (0..V-1)
+  int b_ent;   // a log entry            (term-1 | value << b_tm1)
+  int b_log0;  // a log of <= L entries  (length | entries): voterLog, elog, mlog
+  int b_log1;  // a server's own log     (<= L+1 entries)
+  int b_cnt;   // a message count        (1..C+1)
+  // bit offsets inside a packed record, and its words
+  int sb_log, sb_nm, sb_vl, srv_w;     // server (scalars at bit 0)
+  int eb_log, eb_vl, elec_w;           // election (eterm-1 | eleader | evotes | dom at bit 0)
+  int mb_term, mb_pay, mb_cnt, slot_w; // message (type at bit 0, msource 2, mdest)
 };
+
+constexpr int bits_for(int x) {  // bits to hold 0..x
+  int b = 0;
+  while ((1 << b) <= x) b++;
+  return b;
+}
 
 // Returns 0 on success, <0 if the configuration exceeds the row format.
 constexpr int make_layout(Layout* l, int N, int V, int T, int L, int C, int M, int K, int E, int inv_mask) {
@@ -115,14 +154,46 @@ constexpr int make_layout(Layout* l, int N, int V, int T, int L, int C, int M, i
   for (int n = 0; n <= L + 1; n++) { l->log_off[n] = off; off += pw; pw *= B; }
   l->n_logs = l->log_off[L + 1];
   if (l->n_logs > 32 * 32) return -1;
+  // field widths
+  l->b_tcur = bits_for(T);
+  l->b_tm1 = bits_for(T - 1);
+  l->b_t0 = bits_for(T);
+  l->b_vote = bits_for(N);
+  l->b_sid = bits_for(N - 1);
+  l->b_idx = bits_for(L);
+  l->b_val = bits_for(V - 1);
+  l->b_ent = l->b_tm1 + l->b_val;
+  l->b_log0 = bits_for(L) + L * l->b_ent;
+  l->b_log1 = bits_for(L + 1) + (L + 1) * l->b_ent;
+  l->b_cnt = bits_for(C + 1);
+  // server: scalars | own log | N x (nextIndex-1, matchIndex) | N x voterLog
+  l->sb_log = l->b_tcur + 2 + l->b_vote + l->b_idx + 3 * N;
+  l->sb_nm = l->sb_log + l->b_log1;
+  l->sb_vl = l->sb_nm + 2 * N * l->b_idx;
+  l->srv_w = (l->sb_vl + N * l->b_log0 + 31) / 32;
+  // election: eterm-1 | eleader | evotes | dom | elog | N x evoterLog
+  l->eb_log = l->b_tm1 + l->b_sid + 2 * N;
+  l->eb_vl = l->eb_log + l->b_log0;
+  l->elec_w = (l->eb_vl + N * l->b_log0 + 31) / 32;
+  // message: type | msource | mdest | mterm-1 | payload (the largest type's) | count
+  l->mb_term = 2 + 2 * l->b_sid;
+  l->mb_pay = l->mb_term + l->b_tm1;
+  int pay = l->b_t0 + l->b_idx;                                                      // RVReq
+  if (1 + l->b_log0 > pay) pay = 1 + l->b_log0;                                      // RVResp
+  const int ae = l->b_idx + l->b_t0 + 1 + l->b_ent + l->b_idx + l->b_log0;             // AEReq
+  if (ae > pay) pay = ae;
+  if (1 + l->b_idx > pay) pay = 1 + l->b_idx;                                        // AEResp
+  l->mb_cnt = l->mb_pay + pay;
+  l->slot_w = (l->mb_cnt + l->b_cnt + 31) / 32;
+  if (l->slot_w > 2 || l->srv_w > 6 || l->elec_w > 6) return -1;  // (PACKW)
+  // row
   l->off_hdr = 4;
   l->off_srv = 5;
-  l->off_all = l->off_srv + N * l->SW;
+  l->off_all = l->off_srv + N * l->srv_w;
   l->all_words = (l->n_logs + 31) / 32;
   l->off_elec = l->off_all + l->all_words;
-  l->off_bag = l->off_elec + E * l->EW;
-  l->off_bag += (l->off_bag & 1);  // u64-align the bag
-  l->W = l->off_bag + 2 * K;
+  l->off_bag = l->off_elec + E * l->elec_w;
+  l->W = l->off_bag + K * l->slot_w;
   l->W += !(l->W & 1);  // odd row stride: conflict-free LDS row staging
   int f = 0;
   l->fam[F_RESTART] = f; f += N;
@@ -331,15 +402,206 @@ RTLA_HD FP h_srv(int i, const uint32_t* rec, int SW) {
   }
   return s;
 }
+// A message with its count, as its PACKED slot value (msg_pack: a bijection of
+// the model's message values, so the fingerprint stays a function of the
+// state's value); 0 = empty slot.
 RTLA_HD FP h_msg(uint64_t slot) { return slot ? hash_u64(TAG_MSG, slot) : FP{0, 0}; }
 RTLA_HD FP h_all(int idx) { return hash_u64(TAG_ALL, (uint64_t)idx); }
 RTLA_HD FP h_elec(const uint32_t* rec, int EW) { return hash_words(TAG_ELEC, rec, EW); }
 
 // ------------------------------------------------------------ row I/O ----
+// Bit fields of a packed row (widths <= 32; a field may straddle two words).
 template <class P>
-RTLA_HD uint64_t bag_slot(const Layout& L, P row, int k) {
-  return (uint64_t)row[L.off_bag + 2 * k] | (uint64_t)row[L.off_bag + 2 * k + 1] << 32;
+RTLA_HD uint32_t row_bits(P row, int word, int bit, int nbits) {
+  if (nbits == 0) return 0u;
+  const int w = word + (bit >> 5), s = bit & 31;
+  uint64_t x = (uint64_t)row[w];
+  if (s + nbits > 32) x |= (uint64_t)row[w + 1] << 32;
+  return (uint32_t)(x >> s) & (uint32_t)((1ull << nbits) - 1ull);
 }
+// Packing into a record's words (out: zeroed, enough words).
+RTLA_HD void put_bits(uint32_t* out, int bit, int nbits, uint32_t v) {
+  if (nbits == 0) return;
+  const int w = bit >> 5, s = bit & 31;
+  const uint64_t x = (uint64_t)(v & (uint32_t)((1ull << nbits) - 1ull)) << s;
+  out[w] |= (uint32_t)x;
+  if (s + nbits > 32) out[w + 1] |= (uint32_t)(x >> 32);
+}
+
+// Logs: wide code <-> packed (length | entries, entry = term-1 | value << b_tm1).
+RTLA_HD uint32_t log_pack(const Layout& L, uint32_t code, int lenbits) {
+  const uint32_t n = log_len(code);
+  uint32_t x = n;
+  for (uint32_t k = 1; k <= n; k++)
+    x |= ((log_term(code, k) - 1u) | log_val(code, k) << L.b_tm1) << (lenbits + (int)(k - 1) * L.b_ent);
+  return x;
+}
+RTLA_HD uint32_t log_unpack(const Layout& L, uint32_t x, int lenbits) {
+  const uint32_t n = lenbits ? x & ((1u << lenbits) - 1u) : 0u;
+  uint32_t code = n;
+  for (uint32_t k = 1; k <= n; k++) {
+    const uint32_t e = (x >> (lenbits + (int)(k - 1) * L.b_ent)) & ((1u << L.b_ent) - 1u);
+    const uint32_t term = (e & ((1u << L.b_tm1) - 1u)) + 1u, val = e >> L.b_tm1;
+    code |= (term | val << 3) << (3 + 5 * (k - 1));
+  }
+  return code;
+}
+RTLA_HD int lenbits0(const Layout& L) { return L.b_log0 - L.L * L.b_ent; }
+RTLA_HD int lenbits1(const Layout& L) { return L.b_log1 - (L.L + 1) * L.b_ent; }
+
+// Server record i: the wide words from the packed row.
+template <class P>
+RTLA_HD uint32_t srv_w0(const Layout& L, P row, int i) {
+  const int base = L.off_srv + i * L.srv_w;
+  int b = 0;
+  const uint32_t term = row_bits(row, base, b, L.b_tcur) + 1u; b += L.b_tcur;
+  const uint32_t role = row_bits(row, base, b, 2); b += 2;
+  uint32_t voted = row_bits(row, base, b, L.b_vote); b += L.b_vote;
+  if (voted == (uint32_t)L.N) voted = NIL;
+  const uint32_t commit = row_bits(row, base, b, L.b_idx); b += L.b_idx;
+  const uint32_t masks = row_bits(row, base, b, 3 * L.N);
+  const uint32_t m = (1u << L.N) - 1u;
+  return s_make(term, role, voted, commit, masks & m, (masks >> L.N) & m, (masks >> (2 * L.N)) & m);
+}
+template <class P>
+RTLA_HD uint32_t srv_log(const Layout& L, P row, int i) {
+  return log_unpack(L, row_bits(row, L.off_srv + i * L.srv_w, L.sb_log, L.b_log1), lenbits1(L));
+}
+template <class P>
+RTLA_HD uint32_t srv_nm(const Layout& L, P row, int i) {
+  const int base = L.off_srv + i * L.srv_w;
+  uint32_t nm = 0;
+  for (int j = 0; j < L.N; j++) {
+    const uint32_t x = row_bits(row, base, L.sb_nm + 2 * j * L.b_idx, 2 * L.b_idx);
+    nm |= ((x & ((1u << L.b_idx) - 1u)) + 1u) << (3 * j) | (x >> L.b_idx) << (15 + 3 * j);
+  }
+  return nm;
+}
+template <class P>
+RTLA_HD uint32_t srv_vl(const Layout& L, P row, int i, int j) {
+  return log_unpack(L, row_bits(row, L.off_srv + i * L.srv_w, L.sb_vl + j * L.b_log0, L.b_log0), lenbits0(L));
+}
+// Packed words of a wide server record (out: srv_w words).
+RTLA_HD void srv_pack(const Layout& L, const uint32_t* rec, uint32_t* out) {
+  for (int w = 0; w < L.srv_w; w++) out[w] = 0;
+  const uint32_t w0 = rec[0];
+  int b = 0;
+  put_bits(out, b, L.b_tcur, s_term(w0) - 1u); b += L.b_tcur;
+  put_bits(out, b, 2, s_role(w0)); b += 2;
+  put_bits(out, b, L.b_vote, s_voted(w0) == NIL ? (uint32_t)L.N : s_voted(w0)); b += L.b_vote;
+  put_bits(out, b, L.b_idx, s_commit(w0)); b += L.b_idx;
+  put_bits(out, b, 3 * L.N, s_vresp(w0) | s_vgrant(w0) << L.N | s_vlp(w0) << (2 * L.N));
+  put_bits(out, L.sb_log, L.b_log1, log_pack(L, rec[1], lenbits1(L)));
+  for (int j = 0; j < L.N; j++) {
+    put_bits(out, L.sb_nm + 2 * j * L.b_idx, L.b_idx, nm_next(rec[2], j) - 1u);
+    put_bits(out, L.sb_nm + (2 * j + 1) * L.b_idx, L.b_idx, nm_match(rec[2], j));
+    put_bits(out, L.sb_vl + j * L.b_log0, L.b_log0, log_pack(L, rec[3 + j], lenbits0(L)));
+  }
+}
+
+// Election record e: wide words from the packed row, and back.
+template <class P>
+RTLA_HD uint32_t elec_w0(const Layout& L, P row, int e) {
+  const int base = L.off_elec + e * L.elec_w;
+  const uint32_t x = row_bits(row, base, 0, L.b_tm1 + L.b_sid + 2 * L.N);
+  const uint32_t term = (x & ((1u << L.b_tm1) - 1u)) + 1u;
+  const uint32_t rest = x >> L.b_tm1;
+  const uint32_t leader = rest & ((1u << L.b_sid) - 1u);
+  const uint32_t masks = rest >> L.b_sid, m = (1u << L.N) - 1u;
+  return term | leader << 4 | (masks & m) << 7 | ((masks >> L.N) & m) << 12;
+}
+template <class P>
+RTLA_HD uint32_t elec_log(const Layout& L, P row, int e) {
+  return log_unpack(L, row_bits(row, L.off_elec + e * L.elec_w, L.eb_log, L.b_log0), lenbits0(L));
+}
+template <class P>
+RTLA_HD uint32_t elec_vl(const Layout& L, P row, int e, int j) {
+  return log_unpack(L, row_bits(row, L.off_elec + e * L.elec_w, L.eb_vl + j * L.b_log0, L.b_log0), lenbits0(L));
+}
+RTLA_HD void elec_pack(const Layout& L, const uint32_t* er, uint32_t* out) {
+  for (int w = 0; w < L.elec_w; w++) out[w] = 0;
+  const uint32_t w0 = er[0];
+  put_bits(out, 0, L.b_tm1, (w0 & 15u) - 1u);
+  put_bits(out, L.b_tm1, L.b_sid, (w0 >> 4) & 7u);
+  put_bits(out, L.b_tm1 + L.b_sid, 2 * L.N, ((w0 >> 7) & 31u) | ((w0 >> 12) & 31u) << L.N);
+  put_bits(out, L.eb_log, L.b_log0, log_pack(L, er[1], lenbits0(L)));
+  for (int j = 0; j < L.N; j++) put_bits(out, L.eb_vl + j * L.b_log0, L.b_log0, log_pack(L, er[2 + j], lenbits0(L)));
+}
+
+// Messages: wide value (key | count << 60) <-> packed slot (0 = empty).
+RTLA_HD uint64_t msg_pack(const Layout& L, uint64_t v) {
+  if (!v) return 0ull;
+  uint32_t out[2] = {0u, 0u};
+  const uint32_t type = m_type(v);
+  put_bits(out, 0, 2, type);
+  put_bits(out, 2, L.b_sid, m_src(v));
+  put_bits(out, 2 + L.b_sid, L.b_sid, m_dst(v));
+  put_bits(out, L.mb_term, L.b_tm1, m_term(v) - 1u);
+  int b = L.mb_pay;
+  if (type == RVREQ) {
+    put_bits(out, b, L.b_t0, m_f(v, 12, 4)); b += L.b_t0;
+    put_bits(out, b, L.b_idx, m_f(v, 16, 3));
+  } else if (type == RVRESP) {
+    put_bits(out, b, 1, m_f(v, 12, 1)); b += 1;
+    put_bits(out, b, L.b_log0, log_pack(L, m_f(v, 16, 28), lenbits0(L)));
+  } else if (type == AEREQ) {
+    put_bits(out, b, L.b_idx, m_f(v, 12, 3)); b += L.b_idx;
+    put_bits(out, b, L.b_t0, m_f(v, 15, 4)); b += L.b_t0;
+    const uint32_t has = m_f(v, 19, 1), ent = m_f(v, 20, 5);
+    put_bits(out, b, 1, has); b += 1;
+    put_bits(out, b, L.b_ent, has ? ((ent & 7u) - 1u) | (ent >> 3) << L.b_tm1 : 0u); b += L.b_ent;
+    put_bits(out, b, L.b_idx, m_f(v, 25, 3)); b += L.b_idx;
+    put_bits(out, b, L.b_log0, log_pack(L, m_f(v, 28, 28), lenbits0(L)));
+  } else {
+    put_bits(out, b, 1, m_f(v, 12, 1)); b += 1;
+    put_bits(out, b, L.b_idx, m_f(v, 13, 3));
+  }
+  put_bits(out, L.mb_cnt, L.b_cnt, m_count(v));
+  return (uint64_t)out[0] | (uint64_t)out[1] << 32;
+}
+RTLA_HD uint64_t msg_unpack(const Layout& L, uint64_t x) {
+  if (!x) return 0ull;
+  const uint32_t p[2] = {(uint32_t)x, (uint32_t)(x >> 32)};
+  const uint32_t type = row_bits(p, 0, 0, 2);
+  const uint32_t src = row_bits(p, 0, 2, L.b_sid), dst = row_bits(p, 0, 2 + L.b_sid, L.b_sid);
+  const uint32_t term = row_bits(p, 0, L.mb_term, L.b_tm1) + 1u;
+  int b = L.mb_pay;
+  uint64_t key;
+  if (type == RVREQ) {
+    const uint32_t llt = row_bits(p, 0, b, L.b_t0);
+    key = m_rvreq(src, dst, term, llt, row_bits(p, 0, b + L.b_t0, L.b_idx));
+  } else if (type == RVRESP) {
+    key = m_rvresp(src, dst, term, row_bits(p, 0, b, 1), log_unpack(L, row_bits(p, 0, b + 1, L.b_log0), lenbits0(L)));
+  } else if (type == AEREQ) {
+    const uint32_t prev = row_bits(p, 0, b, L.b_idx); b += L.b_idx;
+    const uint32_t prevt = row_bits(p, 0, b, L.b_t0); b += L.b_t0;
+    const uint32_t has = row_bits(p, 0, b, 1); b += 1;
+    const uint32_t e = row_bits(p, 0, b, L.b_ent); b += L.b_ent;
+    const uint32_t ent = has ? ((e & ((1u << L.b_tm1) - 1u)) + 1u) | (e >> L.b_tm1) << 3 : 0u;
+    const uint32_t commit = row_bits(p, 0, b, L.b_idx); b += L.b_idx;
+    key = m_aereq(src, dst, term, prev, prevt, has, ent, commit, log_unpack(L, row_bits(p, 0, b, L.b_log0), lenbits0(L)));
+  } else {
+    key = m_aeresp(src, dst, term, row_bits(p, 0, b, 1), row_bits(p, 0, b + 1, L.b_idx));
+  }
+  return key | (uint64_t)row_bits(p, 0, L.mb_cnt, L.b_cnt) << 60;
+}
+// Bag slot k: packed (slot_raw) or wide (bag_slot).  Lookups compare packed
+// keys (key_raw: the key packed with its count bits cleared) so that only a
+// found message is ever unpacked.
+template <class P>
+RTLA_HD uint64_t slot_raw(const Layout& L, P row, int k) {
+  const int w = L.off_bag + k * L.slot_w;
+  return L.slot_w == 1 ? (uint64_t)row[w] : (uint64_t)row[w] | (uint64_t)row[w + 1] << 32;
+}
+template <class P>
+RTLA_HD uint64_t bag_slot(const Layout& L, P row, int k) { return msg_unpack(L, slot_raw(L, row, k)); }
+RTLA_HD uint64_t slot_keymask(const Layout& L) { return (1ull << L.mb_cnt) - 1ull; }
+RTLA_HD uint64_t key_raw(const Layout& L, uint64_t key) { return msg_pack(L, key | 1ull << 60) & slot_keymask(L); }
+RTLA_HD uint32_t raw_count(const Layout& L, uint64_t x) {
+  return (uint32_t)(x >> L.mb_cnt) & ((1u << L.b_cnt) - 1u);
+}
+template <class P>
+RTLA_HD uint32_t slot_type(const Layout& L, P row, int k) { return row[L.off_bag + k * L.slot_w] & 3u; }
 template <class P>
 RTLA_HD int row_nmsg(const Layout& L, P row) { return (int)(row[L.off_hdr] & 255u); }
 template <class P>
@@ -354,23 +616,57 @@ RTLA_HD void row_set_fp(P row, FP f) {
   row[2] = (uint32_t)f.b; row[3] = (uint32_t)(f.b >> 32);
 }
 
+// Whole records in and out of a row (host-side builders: Init, permutations,
+// synthetic states; the kernels patch rows through child_patches).
+template <class P>
+RTLA_HD void srv_get(const Layout& L, P row, int i, uint32_t* rec) {
+  rec[0] = srv_w0(L, row, i);
+  rec[1] = srv_log(L, row, i);
+  rec[2] = srv_nm(L, row, i);
+  for (int j = 0; j < L.N; j++) rec[3 + j] = srv_vl(L, row, i, j);
+}
+template <class P>
+RTLA_HD void srv_put(const Layout& L, P row, int i, const uint32_t* rec) {
+  uint32_t out[8];
+  srv_pack(L, rec, out);
+  for (int w = 0; w < L.srv_w; w++) row[L.off_srv + i * L.srv_w + w] = out[w];
+}
+template <class P>
+RTLA_HD void elec_get(const Layout& L, P row, int e, uint32_t* er) {
+  er[0] = elec_w0(L, row, e);
+  er[1] = elec_log(L, row, e);
+  for (int j = 0; j < L.N; j++) er[2 + j] = elec_vl(L, row, e, j);
+}
+template <class P>
+RTLA_HD void elec_put(const Layout& L, P row, int e, const uint32_t* er) {
+  uint32_t out[8];
+  elec_pack(L, er, out);
+  for (int w = 0; w < L.elec_w; w++) row[L.off_elec + e * L.elec_w + w] = out[w];
+}
+template <class P>
+RTLA_HD void slot_put(const Layout& L, P row, int k, uint64_t v) {
+  const uint64_t x = msg_pack(L, v);
+  row[L.off_bag + k * L.slot_w] = (uint32_t)x;
+  if (L.slot_w > 1) row[L.off_bag + k * L.slot_w + 1] = (uint32_t)(x >> 32);
+}
+
 // Full fingerprint of a row, from scratch (Init, checks).
 template <class P>
 RTLA_HD FP row_fingerprint(const Layout& L, P row) {
   FP f{0, 0};
   uint32_t rec[3 + NMAX];
   for (int i = 0; i < L.N; i++) {
-    for (int w = 0; w < L.SW; w++) rec[w] = row[L.off_srv + i * L.SW + w];
+    srv_get(L, row, i, rec);
     f = fp_add(f, h_srv(i, rec, L.SW));
   }
   int nm = row_nmsg(L, row);
-  for (int k = 0; k < nm; k++) f = fp_add(f, h_msg(bag_slot(L, row, k)));
+  for (int k = 0; k < nm; k++) f = fp_add(f, h_msg(slot_raw(L, row, k)));
   for (int x = 0; x < L.n_logs; x++)
     if (row[L.off_all + (x >> 5)] >> (x & 31) & 1u) f = fp_add(f, h_all(x));
   int ne = row_nelec(L, row);
   uint32_t er[2 + NMAX];
   for (int e = 0; e < ne; e++) {
-    for (int w = 0; w < L.EW; w++) er[w] = row[L.off_elec + e * L.EW + w];
+    elec_get(L, row, e, er);
     f = fp_add(f, h_elec(er, L.EW));
   }
   return f;
@@ -381,11 +677,11 @@ template <class P>
 RTLA_HD void row_init(const Layout& L, P row) {
   for (int w = 0; w < L.W; w++) row[w] = 0;
   for (int i = 0; i < L.N; i++) {
-    uint32_t* r = nullptr;
-    (void)r;
-    row[L.off_srv + i * L.SW + 0] = s_make(1, FOLLOWER, NIL, 0, 0, 0, 0);  // :143-147
-    row[L.off_srv + i * L.SW + 1] = 0;                                     // log = <<>> :153
-    row[L.off_srv + i * L.SW + 2] = nm_fill(L.N, 1, 0);                    // :151-152
+    uint32_t rec[3 + NMAX] = {0};
+    rec[0] = s_make(1, FOLLOWER, NIL, 0, 0, 0, 0);  // :143-147
+    rec[1] = 0;                                     // log = <<>> :153
+    rec[2] = nm_fill(L.N, 1, 0);                    // :151-152
+    srv_put(L, row, i, rec);
   }
   row_set_fp(row, row_fingerprint(L, row));
 }
@@ -409,7 +705,7 @@ struct DeltaT {
   uint32_t rec[3 + NR];    // its new record
   int32_t nops;            // bag slot writes (<= 3)
   int32_t op_slot[3];
-  uint64_t op_old[3], op_new[3];
+  uint64_t op_old[3], op_new[3];  // PACKED slot values (msg_pack; 0 = empty)
   int32_t nmsg;            // new number of bag slots in use
   int32_t elec;            // 1: append erec to elections
   uint32_t erec[2 + NR];
@@ -426,9 +722,10 @@ RTLA_HD void set_at(T* a, int j, T v) {
     if (k == j) a[k] = v;
 }
 
+// DeltaT's bag: slot writes over the parent's slots, all in PACKED form.
 template <class P, int NR>
 RTLA_HD uint64_t bag_get(const Layout& L, P row, const DeltaT<NR>& d, int slot) {
-  uint64_t v = bag_slot(L, row, slot);
+  uint64_t v = slot_raw(L, row, slot);
 #pragma unroll
   for (int q = 0; q < 3; q++)
     if (q < d.nops && d.op_slot[q] == slot) v = d.op_new[q];
@@ -442,45 +739,54 @@ RTLA_HD void bag_set(const Layout& L, P row, DeltaT<NR>& d, int slot, uint64_t v
     if (!done && q < d.nops && d.op_slot[q] == slot) { d.op_new[q] = v; done = true; }
   if (done) return;
   if (d.nops >= 3) { d.err = 2; return; }
-  const uint64_t old = bag_slot(L, row, slot);
+  const uint64_t old = slot_raw(L, row, slot);
 #pragma unroll
   for (int q = 0; q < 3; q++)
     if (q == d.nops) { d.op_slot[q] = slot; d.op_old[q] = old; d.op_new[q] = v; }
   d.nops++;
 }
+// slot holding packed key pk (count bits cleared), or -1
 template <class P, int NR>
-RTLA_HD int bag_find(const Layout& L, P row, const DeltaT<NR>& d, uint64_t key) {
+RTLA_HD int bag_find(const Layout& L, P row, const DeltaT<NR>& d, uint64_t pk) {
+  const uint64_t km = slot_keymask(L);
   int hit = -1;
-  for (int k = 0; k < d.nmsg; k++)
-    if (hit < 0 && m_key(bag_get(L, row, d, k)) == key) hit = k;
+  for (int k = 0; k < d.nmsg; k++) {
+    const uint64_t x = bag_get(L, row, d, k);
+    if (hit < 0 && x != 0 && (x & km) == pk) hit = k;
+  }
   return hit;
 }
+RTLA_HD uint64_t count_one(const Layout& L) { return 1ull << L.mb_cnt; }
 // raft.tla:106-110 WithMessage
 template <class P, int NR>
 RTLA_HD void with_message(const Layout& L, P row, DeltaT<NR>& d, uint64_t key) {
-  int p = bag_find(L, row, d, key);
+  const uint64_t pk = key_raw(L, key);
+  int p = bag_find(L, row, d, pk);
   if (p >= 0) {
-    bag_set(L, row, d, p, bag_get(L, row, d, p) + (1ull << 60));
+    bag_set(L, row, d, p, bag_get(L, row, d, p) + count_one(L));
   } else {
     if (d.nmsg >= L.K) { d.err = 2; return; }
-    bag_set(L, row, d, d.nmsg, key | (1ull << 60));
+    bag_set(L, row, d, d.nmsg, pk | count_one(L));
     d.nmsg++;
   }
 }
-// raft.tla:114-119 WithoutMessage
+// raft.tla:114-119 WithoutMessage, of the message in slot p
 template <class P, int NR>
-RTLA_HD void without_message(const Layout& L, P row, DeltaT<NR>& d, uint64_t key) {
-  int p = bag_find(L, row, d, key);
-  if (p < 0) return;
-  uint64_t v = bag_get(L, row, d, p);
-  if (m_count(v) <= 1) {
+RTLA_HD void without_slot(const Layout& L, P row, DeltaT<NR>& d, int p) {
+  const uint64_t v = bag_get(L, row, d, p);
+  if (raw_count(L, v) <= 1) {
     int last = d.nmsg - 1;
     if (p != last) bag_set(L, row, d, p, bag_get(L, row, d, last));
     bag_set(L, row, d, last, 0);
     d.nmsg--;
   } else {
-    bag_set(L, row, d, p, v - (1ull << 60));
+    bag_set(L, row, d, p, v - count_one(L));
   }
+}
+template <class P, int NR>
+RTLA_HD void without_message(const Layout& L, P row, DeltaT<NR>& d, uint64_t key) {
+  const int p = bag_find(L, row, d, key_raw(L, key));
+  if (p >= 0) without_slot(L, row, d, p);
 }
 
 // Fingerprint-only sink for compute_delta (the BFS probe pass).  The same
@@ -507,52 +813,64 @@ struct DeltaFpT {
 };
 using DeltaFp = DeltaFpT<NMAX>;
 
+// Slot of packed key pk among the first n (parent) slots, its count in *count.
 template <class P>
-RTLA_HD int bag_find0(const Layout& L, P row, int n, uint64_t key, uint64_t* val) {
+RTLA_HD int bag_find0(const Layout& L, P row, int n, uint64_t pk, uint32_t* count) {
+  const uint64_t km = slot_keymask(L);
   int hit = -1;
-  uint64_t v = 0;
+  uint32_t c = 0;
   for (int k = 0; k < n; k++) {
-    const uint64_t x = bag_slot(L, row, k);
-    if (hit < 0 && m_key(x) == key) { hit = k; v = x; }
+    const uint64_t x = slot_raw(L, row, k);
+    if (hit < 0 && x != 0 && (x & km) == pk) { hit = k; c = raw_count(L, x); }
   }
-  *val = v;
+  *count = c;
   return hit;
 }
-// count c -> c + dc of message `key` (c = 0: absent), for the probe pass
+// count c -> c + dc of the message with packed key pk (c = 0: absent), for the probe pass
 template <int NR>
-RTLA_HD void fp_bag_count(const Layout& L, DeltaFpT<NR>& d, uint64_t key, uint32_t c, int dc) {
+RTLA_HD void fp_bag_count(const Layout& L, DeltaFpT<NR>& d, uint64_t pk, uint32_t c, int dc) {
   const uint32_t n = (uint32_t)((int)c + dc);
   if ((int)n > L.C) d.in_model = 0;
   d.dcount += dc;
-  if (c) d.fmsg = fp_sub(d.fmsg, h_msg(key | (uint64_t)c << 60));
-  if (n) d.fmsg = fp_add(d.fmsg, h_msg(key | (uint64_t)n << 60));
+  if (c) d.fmsg = fp_sub(d.fmsg, h_msg(pk | (uint64_t)c << L.mb_cnt));
+  if (n) d.fmsg = fp_add(d.fmsg, h_msg(pk | (uint64_t)n << L.mb_cnt));
 }
 template <class P, int NR>
 RTLA_HD void with_message(const Layout& L, P row, DeltaFpT<NR>& d, uint64_t key) {  // raft.tla:106-110
-  uint64_t v;
-  if (bag_find0(L, row, d.nmsg0, key, &v) >= 0) {
-    fp_bag_count(L, d, key, m_count(v), 1);
+  const uint64_t pk = key_raw(L, key);
+  uint32_t c;
+  if (bag_find0(L, row, d.nmsg0, pk, &c) >= 0) {
+    fp_bag_count(L, d, pk, c, 1);
   } else {
     if (d.nmsg >= L.K) { d.err = 2; return; }
     d.nmsg++;
-    fp_bag_count(L, d, key, 0, 1);
+    fp_bag_count(L, d, pk, 0, 1);
   }
 }
 template <class P, int NR>
+RTLA_HD void without_slot(const Layout& L, P row, DeltaFpT<NR>& d, int x) {  // raft.tla:114-119, slot x
+  const uint64_t v = slot_raw(L, row, x);
+  const uint32_t c = raw_count(L, v);
+  if (c <= 1) d.nmsg--;
+  fp_bag_count(L, d, v & slot_keymask(L), c, -1);
+}
+template <class P, int NR>
 RTLA_HD void without_message(const Layout& L, P row, DeltaFpT<NR>& d, uint64_t key) {  // raft.tla:114-119
-  uint64_t v;
-  if (bag_find0(L, row, d.nmsg0, key, &v) < 0) return;
-  if (m_count(v) <= 1) d.nmsg--;
-  fp_bag_count(L, d, key, m_count(v), -1);
+  const uint64_t pk = key_raw(L, key);
+  uint32_t c;
+  const int x = bag_find0(L, row, d.nmsg0, pk, &c);
+  if (x < 0) return;
+  if (c <= 1) d.nmsg--;
+  fp_bag_count(L, d, pk, c, -1);
 }
 template <class P, int NR>
 RTLA_HD void bag_dup_slot(const Layout& L, P row, DeltaFpT<NR>& d, int x) {  // DuplicateMessage :443-445
-  const uint64_t v = bag_slot(L, row, x);
-  fp_bag_count(L, d, m_key(v), m_count(v), 1);
+  const uint64_t v = slot_raw(L, row, x);
+  fp_bag_count(L, d, v & slot_keymask(L), raw_count(L, v), 1);
 }
 template <class P, int NR>
 RTLA_HD void bag_dup_slot(const Layout& L, P row, DeltaT<NR>& d, int x) {
-  bag_set(L, row, d, x, bag_slot(L, row, x) + (1ull << 60));
+  bag_set(L, row, d, x, slot_raw(L, row, x) + count_one(L));
 }
 template <int NR>
 RTLA_HD void delta_reset(DeltaT<NR>& d) { d.nops = 0; }
@@ -568,14 +886,14 @@ RTLA_HD void bag_constraint(const Layout& L, P row, DeltaT<NR>& d) {
 #pragma unroll
   for (int q = 0; q < 3; q++) {
     if (q < d.nops) {
-      if ((int)m_count(d.op_new[q]) > L.C) d.in_model = 0;
-      total_delta += (int)m_count(d.op_new[q]) - (int)m_count(d.op_old[q]);
+      if ((int)raw_count(L, d.op_new[q]) > L.C) d.in_model = 0;
+      total_delta += (int)raw_count(L, d.op_new[q]) - (int)raw_count(L, d.op_old[q]);
     }
   }
   if (L.M > 0 && total_delta > 0) {
     int total = 0;
     const int nm = row_nmsg(L, row);
-    for (int k = 0; k < nm; k++) total += (int)m_count(bag_slot(L, row, k));
+    for (int k = 0; k < nm; k++) total += (int)raw_count(L, slot_raw(L, row, k));
     if (total + total_delta > L.M) d.in_model = 0;
   }
 }
@@ -583,17 +901,19 @@ template <class P, int NR>
 RTLA_HD void bag_constraint(const Layout& L, P row, DeltaFpT<NR>& d) {
   if (L.M > 0 && d.dcount > 0) {
     int total = 0;
-    for (int k = 0; k < d.nmsg0; k++) total += (int)m_count(bag_slot(L, row, k));
+    for (int k = 0; k < d.nmsg0; k++) total += (int)raw_count(L, slot_raw(L, row, k));
     if (total + d.dcount > L.M) d.in_model = 0;
   }
 }
 
 template <int NS, class P>
 RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
-  const int SW = 3 + RTLA_NSRV(L);
+  rec[0] = srv_w0(L, row, i);
+  rec[1] = srv_log(L, row, i);
+  rec[2] = srv_nm(L, row, i);
 #pragma unroll
-  for (int w = 0; w < 3 + (NS ? NS : NMAX); w++)
-    if (w < SW) rec[w] = row[L.off_srv + i * SW + w];
+  for (int j = 0; j < (NS ? NS : NMAX); j++)
+    if (j < RTLA_NSRV(L)) rec[3 + j] = srv_vl(L, row, i, j);
 }
 
 // Compute the successor of `row` under action instance `inst` (0..L.fam[F_COUNT]).
@@ -603,7 +923,6 @@ RTLA_HD void load_rec(const Layout& L, P row, int i, uint32_t* rec) {
 template <int NS, int FAM = -1, class P, class D>
 RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
   const int N = RTLA_NSRV(L);
-  const int SW = 3 + N;
   d.enabled = 0; d.in_model = 1; d.sub = R_NONE; d.err = 0; d.srv = -1;
   d.nmsg = row_nmsg(L, row); d.elec = 0;
   delta_reset(d);
@@ -637,8 +956,9 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
     if ((int)t > L.T) d.in_model = 0;
   } else if (fam == F_REQUESTVOTE) {            // RequestVote(i, j) :190-199
     const int i = x / N, j = x - (x / N) * N;
-    const uint32_t w0 = row[L.off_srv + i * SW], lg = row[L.off_srv + i * SW + 1];
+    const uint32_t w0 = srv_w0(L, row, i);
     if (s_role(w0) != CANDIDATE || (s_vresp(w0) >> j & 1u)) return;
+    const uint32_t lg = srv_log(L, row, i);
     with_message(L, row, d, m_rvreq(i, j, s_term(w0), last_term(lg), log_len(lg)));
     d.enabled = 1;
   } else if (fam == F_BECOMELEADER) {           // BecomeLeader(i) :229-243
@@ -656,13 +976,12 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
 #pragma unroll
     for (int j = 0; j < (NS ? NS : NMAX); j++) d.erec[2 + j] = j < N ? rec[3 + j] : 0u;
     const int ne = row_nelec(L, row);
-    const int EW = 2 + N;
+    uint32_t pk[8];  // the record packed: equal records have equal packed words
+    elec_pack(L, d.erec, pk);
     int dup = 0;
     for (int e = 0; e < ne; e++) {
       int same = 1;
-#pragma unroll
-      for (int w = 0; w < 2 + (NS ? NS : NMAX); w++)
-        if (w < EW) same &= row[L.off_elec + e * EW + w] == d.erec[w];
+      for (int w = 0; w < L.elec_w; w++) same &= row[L.off_elec + e * L.elec_w + w] == pk[w];
       dup |= same;
     }
     if (!dup) {
@@ -697,9 +1016,9 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
   } else if (fam == F_APPENDENTRIES) {          // AppendEntries(i, j) :204-226
     const int i = x / N, j = x - (x / N) * N;
     if (i == j) return;
-    const uint32_t w0 = row[L.off_srv + i * SW], lg = row[L.off_srv + i * SW + 1];
-    const uint32_t nm = row[L.off_srv + i * SW + 2];
+    const uint32_t w0 = srv_w0(L, row, i);
     if (s_role(w0) != LEADER) return;
+    const uint32_t lg = srv_log(L, row, i), nm = srv_nm(L, row, i);
     const uint32_t nxt = nm_next(nm, j), prev = nxt - 1, len = log_len(lg);
     uint32_t prevt = 0;
     if (prev > 0) {
@@ -736,11 +1055,11 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
         d.srv = i;
       }
       with_message(L, row, d, m_rvresp(i, j, cur, grant ? 1u : 0u, lg));  // Reply :129-130
-      without_message(L, row, d, key);
+      without_slot(L, row, d, x);
       d.enabled = 1; d.sub = R_HRVREQ;
     } else if (type == RVRESP || type == AERESP) {
       if (mt < cur) {                            // DropStaleResponse :415-418
-        without_message(L, row, d, key);
+        without_slot(L, row, d, x);
         d.enabled = 1; d.sub = R_DROPSTALE;
       } else if (type == RVRESP) {               // HandleRequestVoteResponse :307-321
         uint32_t vr = s_vresp(rec[0]) | 1u << j, vg = s_vgrant(rec[0]), vlp = s_vlp(rec[0]);
@@ -752,7 +1071,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
           }
         }
         rec[0] = s_make(cur, role, s_voted(rec[0]), s_commit(rec[0]), vr, vg, vlp);
-        without_message(L, row, d, key);
+        without_slot(L, row, d, x);
         d.srv = i; d.enabled = 1; d.sub = R_HRVRESP;
       } else {                                   // HandleAppendEntriesResponse :393-403
         const uint32_t succ = m_f(key, 12, 1), mm = m_f(key, 13, 3);
@@ -762,7 +1081,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
           const uint32_t nx = nm_next(rec[2], j);
           rec[2] = nm_set_next(rec[2], j, nx > 2 ? nx - 1 : 1);   // Max({next - 1, 1})
         }
-        without_message(L, row, d, key);
+        without_slot(L, row, d, x);
         d.srv = i; d.enabled = 1; d.sub = R_HAERESP;
       }
     } else {                                     // HandleAppendEntriesRequest :327-389
@@ -771,7 +1090,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
       const int logok = prev == 0 || (prev > 0 && prev <= len && prevt == log_term(lg, prev));
       if (mt < cur || (mt == cur && role == FOLLOWER && !logok)) {   // reject :333-345
         with_message(L, row, d, m_aeresp(i, j, cur, 0, 0));
-        without_message(L, row, d, key);
+        without_slot(L, row, d, x);
         d.enabled = 1; d.sub = R_HAEREQ;
       } else if (mt == cur && role == CANDIDATE) {                  // return to follower :346-350
         rec[0] = (rec[0] & ~(3u << 4)) | (FOLLOWER << 4);
@@ -782,7 +1101,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
           rec[0] = (rec[0] & ~(7u << 9)) | mci << 9;
           d.srv = i;
           with_message(L, row, d, m_aeresp(i, j, cur, 1, prev + has));
-          without_message(L, row, d, key);
+          without_slot(L, row, d, x);
           d.enabled = 1; d.sub = R_HAEREQ;
         } else if (len >= index) {               // conflict: remove 1 entry :375-382
           rec[1] = log_prefix(lg, len - 1);
@@ -800,7 +1119,7 @@ RTLA_HD void compute_delta(const Layout& L, P row, int inst, D& d) {
     d.enabled = 1;
   } else {                                      // DropMessage(m) :448-450
     if (x >= d.nmsg) return;
-    without_message(L, row, d, m_key(bag_slot(L, row, x)));
+    without_slot(L, row, d, x);
     d.enabled = 1;
   }
   if (!d.enabled) return;
@@ -858,11 +1177,11 @@ RTLA_HD FP delta_fp(const Layout& L, P row, const DeltaFpT<NR>& d, const FP* h_o
 // Writes the new allLogs words into all_out and returns the fingerprint change.
 template <int NS, class P, class Q>
 RTLA_HD FP alllogs_delta(const Layout& L, P row, Q all_out) {
-  const int N = RTLA_NSRV(L), SW = 3 + N;
+  const int N = RTLA_NSRV(L);
   FP f{0, 0};
   for (int w = 0; w < L.all_words; w++) all_out[w] = row[L.off_all + w];
   for (int i = 0; i < N; i++) {
-    const int x = log_index(L, row[L.off_srv + i * SW + 1]);
+    const int x = log_index(L, srv_log(L, row, i));
     const uint32_t bit = 1u << (x & 31);
     if (!(all_out[x >> 5] & bit)) {
       all_out[x >> 5] |= bit;
@@ -875,34 +1194,45 @@ RTLA_HD FP alllogs_delta(const Layout& L, P row, Q all_out) {
 // The words in which the successor row (parent + delta, with the new allLogs
 // words and fingerprint) differs from its parent row, as put(word, value)
 // calls; every other word of the child equals the parent's.  At most
-// 4 + 1 + SW + all_words + EW + 6 words.
-template <int NS, class P, class R, class F, int NR>
-RTLA_HD void child_patches(const Layout& L, P row, const DeltaT<NR>& d, R all_new, FP fp, F put) {
-  const int SW = 3 + RTLA_NSRV(L), EW = 2 + RTLA_NSRV(L);
+// 4 + 1 + srv_w + all_words + elec_w + 3 * slot_w words.  In two steps:
+// child_pack packs the delta's changed records (after which the wide
+// records are dead: the kernels pack before they wait for the parent-row
+// copies, and keep only the packed words across the wait), child_write
+// emits the words.
+constexpr int PACKW = 6;  // words of a packed server / election record, at most (make_layout)
+template <int NR>
+RTLA_HD void child_pack(const Layout& L, const DeltaT<NR>& d, uint32_t* spk, uint32_t* epk) {
+  if (d.srv >= 0) srv_pack(L, d.rec, spk);
+  if (d.elec) elec_pack(L, d.erec, epk);
+}
+template <class P, class R, class F, int NR>
+RTLA_HD void child_write(const Layout& L, P row, const DeltaT<NR>& d, const uint32_t* spk, const uint32_t* epk,
+                         R all_new, FP fp, F put) {
   put(0, (uint32_t)fp.a);
   put(1, (uint32_t)(fp.a >> 32));
   put(2, (uint32_t)fp.b);
   put(3, (uint32_t)(fp.b >> 32));
   const int ne = row_nelec(L, row) + (d.elec ? 1 : 0);
   put(L.off_hdr, (uint32_t)d.nmsg | (uint32_t)ne << 8);
-  if (d.srv >= 0) {
-#pragma unroll
-    for (int w = 0; w < 3 + (NS ? NS : NMAX); w++)
-      if (w < SW) put(L.off_srv + d.srv * SW + w, d.rec[w]);
-  }
+  if (d.srv >= 0)
+    for (int w = 0; w < L.srv_w; w++) put(L.off_srv + d.srv * L.srv_w + w, spk[w]);
   for (int w = 0; w < L.all_words; w++) put(L.off_all + w, all_new[w]);
-  if (d.elec) {
-#pragma unroll
-    for (int w = 0; w < 2 + (NS ? NS : NMAX); w++)
-      if (w < EW) put(L.off_elec + (ne - 1) * EW + w, d.erec[w]);
-  }
+  if (d.elec)
+    for (int w = 0; w < L.elec_w; w++) put(L.off_elec + (ne - 1) * L.elec_w + w, epk[w]);
 #pragma unroll
   for (int q = 0; q < 3; q++) {
     if (q < d.nops) {
-      put(L.off_bag + 2 * d.op_slot[q], (uint32_t)d.op_new[q]);
-      put(L.off_bag + 2 * d.op_slot[q] + 1, (uint32_t)(d.op_new[q] >> 32));
+      const uint64_t x = d.op_new[q];  // packed
+      put(L.off_bag + d.op_slot[q] * L.slot_w, (uint32_t)x);
+      if (L.slot_w > 1) put(L.off_bag + d.op_slot[q] * L.slot_w + 1, (uint32_t)(x >> 32));
     }
   }
+}
+template <int NS, class P, class R, class F, int NR>
+RTLA_HD void child_patches(const Layout& L, P row, const DeltaT<NR>& d, R all_new, FP fp, F put) {
+  uint32_t spk[PACKW], epk[PACKW];
+  child_pack(L, d, spk, epk);
+  child_write(L, row, d, spk, epk, all_new, fp, put);
 }
 
 // Materialise the successor row: child = parent + child_patches.
@@ -1012,9 +1342,12 @@ RTLA_HD void perm_srv_rec(const uint32_t* rec, const int* pi, const int* inv, ui
   out[2] = nm;
 }
 template <int NS>
-RTLA_HD uint64_t perm_msg_slot(uint64_t v, const int* pi) {  // msource bits 2-4, mdest bits 5-7
+RTLA_HD uint64_t perm_msg_slot(const Layout& L, uint64_t v, const int* pi) {  // a PACKED slot relabelled
   if (!v) return 0;  // empty slot (h_msg(0) = 0)
-  return (v & ~(63ull << 2)) | (uint64_t)perm_id<NS>(m_src(v), pi) << 2 | (uint64_t)perm_id<NS>(m_dst(v), pi) << 5;
+  const uint64_t m = (1ull << L.b_sid) - 1ull;
+  const uint32_t src = (uint32_t)(v >> 2 & m), dst = (uint32_t)(v >> (2 + L.b_sid) & m);
+  return (v & ~(m << 2 | m << (2 + L.b_sid))) | (uint64_t)perm_id<NS>(src, pi) << 2 |
+         (uint64_t)perm_id<NS>(dst, pi) << (2 + L.b_sid);
 }
 template <int NS>
 RTLA_HD void perm_elec(const uint32_t* e, const int* pi, const int* inv, uint32_t* out) {
@@ -1071,12 +1404,13 @@ RTLA_HD FP orbit_key_finish(FP m) {
 
 // The orbit key of a state given through accessors:
 //   rec_of(i, out)  server i's record (3 + NS words)
-//   slot_of(q)      bag slot q < nmsg (0 = empty)
+//   slot_of(q)      bag slot q < nmsg, PACKED (0 = empty)
 //   elec_of(e, out) election record e < nelec (2 + NS words)
 //   afp             fingerprint of allLogs (permutation-free)
 // `perms` (optional) receives |C(s)|.
 template <int NS, class RecF, class SlotF, class ElecF>
-RTLA_HD FP sym_key(RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp, int* perms = nullptr) {
+RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
+                   int* perms = nullptr) {
   constexpr int SW = 3 + NS, EW = 2 + NS;
   // signatures: local part (high half) | sent/received message multisets
   uint32_t ms[NS], mr[NS];
@@ -1086,8 +1420,9 @@ RTLA_HD FP sym_key(RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_o
   for (int q = 0; q < nmsg; q++) {
     const uint64_t v = slot_of(q);
     if (!v) continue;
-    const uint32_t src = m_src(v), dst = m_dst(v);
-    const uint64_t anon = v & ~(63ull << 2);  // names dropped (msource /= mdest in every message)
+    const uint64_t sm = (1ull << L.b_sid) - 1ull;
+    const uint32_t src = (uint32_t)(v >> 2 & sm), dst = (uint32_t)(v >> (2 + L.b_sid) & sm);
+    const uint64_t anon = v & ~(sm << 2 | sm << (2 + L.b_sid));  // names dropped (msource /= mdest in every message)
     const uint32_t c = mix32((uint32_t)anon ^ mix32((uint32_t)(anon >> 32) + 0x632be5abu));
     const uint32_t cr = mix32(c ^ 0x5bd1e995u);
 #pragma unroll
@@ -1157,7 +1492,7 @@ RTLA_HD FP sym_key(RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_o
       perm_srv_rec<NS>(rec, pi, inv, out);
       f = fp_add(f, hash_words_from<SW>(srv_seed<NS>(pi[i]), out));
     }
-    for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot<NS>(slot_of(q), pi)));
+    for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot<NS>(L, slot_of(q), pi)));
     for (int e = 0; e < nelec; e++) {
       uint32_t er[EW], out[EW];
       elec_of(e, er);
@@ -1187,11 +1522,10 @@ RTLA_HD FP alllogs_fp(const Layout& L, Q words) {
 // Orbit key of a materialised row (host: rtla_orbit_key, tests).
 template <int NS, class P>
 RTLA_HD FP orbit_key_row(const Layout& L, P row, int* perms = nullptr) {
-  constexpr int EW = 2 + NS;
-  return sym_key<NS>([&](int i, uint32_t* out) { load_rec<NS>(L, row, i, out); }, row_nmsg(L, row),
-                     [&](int q) { return bag_slot(L, row, q); }, row_nelec(L, row),
+  return sym_key<NS>(L, [&](int i, uint32_t* out) { load_rec<NS>(L, row, i, out); }, row_nmsg(L, row),
+                     [&](int q) { return slot_raw(L, row, q); }, row_nelec(L, row),
                      [&](int e, uint32_t* out) {
-                       for (int w = 0; w < EW; w++) out[w] = row[L.off_elec + e * EW + w];
+                       elec_get(L, row, e, out);
                      },
                      alllogs_fp(L, row + L.off_all), perms);
 }
@@ -1211,19 +1545,19 @@ RTLA_HD void permute_row(const Layout& L, P row, const int* pi, Q out) {
     uint32_t rec[SW], img[SW];
     load_rec<NS>(L, row, i, rec);
     perm_srv_rec<NS>(rec, pi, inv, img);
-    for (int w = 0; w < SW; w++) out[L.off_srv + pi[i] * SW + w] = img[w];
+    srv_put(L, out, pi[i], img);
   }
   const int nm = row_nmsg(L, row), ne = row_nelec(L, row);
   for (int q = 0; q < nm; q++) {
-    const uint64_t v = perm_msg_slot<NS>(bag_slot(L, row, q), pi);
-    out[L.off_bag + 2 * q] = (uint32_t)v;
-    out[L.off_bag + 2 * q + 1] = (uint32_t)(v >> 32);
+    const uint64_t x = perm_msg_slot<NS>(L, slot_raw(L, row, q), pi);
+    out[L.off_bag + q * L.slot_w] = (uint32_t)x;
+    if (L.slot_w > 1) out[L.off_bag + q * L.slot_w + 1] = (uint32_t)(x >> 32);
   }
   for (int e = 0; e < ne; e++) {
     uint32_t er[EW], img[EW];
-    for (int w = 0; w < EW; w++) er[w] = row[L.off_elec + e * EW + w];
+    elec_get(L, row, e, er);
     perm_elec<NS>(er, pi, inv, img);
-    for (int w = 0; w < EW; w++) out[L.off_elec + e * EW + w] = img[w];
+    elec_put(L, out, e, img);
   }
   row_set_fp(out, row_fingerprint(L, out));
 }
@@ -1235,14 +1569,14 @@ RTLA_HD void permute_row(const Layout& L, P row, const int* pi, Q out) {
 template <int NS, class P>
 RTLA_HD int check_invariants_v(const Layout& L, P row, int dsrv, uint32_t drec0, uint32_t drec1, int delec,
                                uint32_t derec0) {
-  const int N = RTLA_NSRV(L), SW = 3 + N, EW = 2 + N;
+  const int N = RTLA_NSRV(L);
   constexpr int NC = NS ? NS : NMAX;
   int bad = 0;
   uint32_t w0[NC], lg[NC];
 #pragma unroll
   for (int i = 0; i < NC; i++) {
-    w0[i] = i < N ? row[L.off_srv + i * SW] : 0u;
-    lg[i] = i < N ? row[L.off_srv + i * SW + 1] : 0u;
+    w0[i] = i < N ? srv_w0(L, row, i) : 0u;
+    lg[i] = i < N ? srv_log(L, row, i) : 0u;
     if (i == dsrv) { w0[i] = drec0; lg[i] = drec1; }
   }
   if (L.inv_mask & INV_NO_TWO_LEADERS) {
@@ -1257,9 +1591,9 @@ RTLA_HD int check_invariants_v(const Layout& L, P row, int dsrv, uint32_t drec0,
     const int ne = row_nelec(L, row);
     const int tot = ne + (delec ? 1 : 0);
     for (int a = 0; a < tot; a++) {
-      const uint32_t ea = a < ne ? row[L.off_elec + a * EW] : derec0;
+      const uint32_t ea = a < ne ? elec_w0(L, row, a) : derec0;
       for (int b = a + 1; b < tot; b++) {
-        const uint32_t eb = b < ne ? row[L.off_elec + b * EW] : derec0;
+        const uint32_t eb = b < ne ? elec_w0(L, row, b) : derec0;
         if ((ea & 15u) == (eb & 15u) && ((ea >> 4) & 7u) != ((eb >> 4) & 7u)) bad |= INV_ELECTION_SAFETY;
       }
     }

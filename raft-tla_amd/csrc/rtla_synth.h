@@ -53,47 +53,49 @@ RTLA_HD uint32_t synth_log(const Layout& L, SynthRng& g, uint32_t maxlen) {
 template <class P>
 RTLA_HD void random_state(const Layout& L, uint64_t seed, uint64_t id, P row) {
   SynthRng g{mix_b(seed * 0x9E3779B97F4A7C15ull ^ mix_a(id + 0x243f6a8885a308d3ull)), 0};
-  const int N = L.N, SW = L.SW, EW = L.EW;
+  const int N = L.N, EW = L.EW;
   const uint32_t all_srv = (1u << N) - 1u;
   for (int w = 0; w < L.W; w++) row[w] = 0;
   for (int i = 0; i < N; i++) {
+    uint32_t rec[3 + NMAX] = {0};
     const uint32_t lg = synth_log(L, g, (uint32_t)L.L);
     const uint32_t len = log_len(lg);
     const uint32_t vresp = g.below(all_srv + 1);
     const uint32_t vgrant = vresp & g.below(all_srv + 1);
     const uint32_t vlp = vgrant & g.below(all_srv + 1);
     const uint32_t voted = g.below((uint32_t)N + 1);
-    row[L.off_srv + i * SW + 0] =
-        s_make(1 + g.below((uint32_t)L.T), g.below(3), voted == (uint32_t)N ? NIL : voted, g.below(len + 1), vresp,
-               vgrant, vlp);
-    row[L.off_srv + i * SW + 1] = lg;
+    rec[0] = s_make(1 + g.below((uint32_t)L.T), g.below(3), voted == (uint32_t)N ? NIL : voted, g.below(len + 1), vresp,
+                    vgrant, vlp);
+    rec[1] = lg;
     uint32_t nm = 0;
     for (int j = 0; j < N; j++) {
       nm = nm_set_next(nm, j, 1 + g.below(len + 1));
       nm = nm_set_match(nm, j, g.below((uint32_t)L.L + 1));
     }
-    row[L.off_srv + i * SW + 2] = nm;
+    rec[2] = nm;
     for (int j = 0; j < N; j++)
-      if (vlp >> j & 1u) row[L.off_srv + i * SW + 3 + j] = synth_log(L, g, (uint32_t)L.L);
+      if (vlp >> j & 1u) rec[3 + j] = synth_log(L, g, (uint32_t)L.L);
+    srv_put(L, row, i, rec);
   }
   for (int x = 0; x < L.n_logs; x++)
     if (g.below(16) == 0) row[L.off_all + (x >> 5)] |= 1u << (x & 31);
   int ne = 0;
   const int want_e = (int)g.below((uint32_t)L.E);  // < E: BecomeLeader may still append one
   for (int e = 0; e < want_e; e++) {
-    uint32_t er[2 + NMAX];
+    uint32_t er[2 + NMAX], have[2 + NMAX];
     const uint32_t votes = g.below(all_srv + 1), dom = votes & g.below(all_srv + 1);
     er[0] = (1 + g.below((uint32_t)L.T)) | g.below((uint32_t)N) << 4 | votes << 7 | dom << 12;
     er[1] = synth_log(L, g, (uint32_t)L.L);
     for (int j = 0; j < N; j++) er[2 + j] = (dom >> j & 1u) ? synth_log(L, g, (uint32_t)L.L) : 0u;
     bool dup = false;
     for (int f = 0; f < ne; f++) {
+      elec_get(L, row, f, have);
       bool same = true;
-      for (int w = 0; w < EW; w++) same = same && row[L.off_elec + f * EW + w] == er[w];
+      for (int w = 0; w < EW; w++) same = same && have[w] == er[w];
       dup = dup || same;
     }
     if (dup) continue;
-    for (int w = 0; w < EW; w++) row[L.off_elec + ne * EW + w] = er[w];
+    elec_put(L, row, ne, er);
     ne++;
   }
   int nmsg = 0;
@@ -115,11 +117,10 @@ RTLA_HD void random_state(const Layout& L, uint64_t seed, uint64_t id, P row) {
       key = m_aeresp(src, dst, term, g.below(2), g.below((uint32_t)L.L + 1));
     }
     bool dup = false;
-    for (int k = 0; k < nmsg; k++) dup = dup || m_key(bag_slot(L, row, k)) == key;
+    const uint64_t pk = key_raw(L, key);
+    for (int k = 0; k < nmsg; k++) dup = dup || (slot_raw(L, row, k) & slot_keymask(L)) == pk;
     if (dup) continue;
-    const uint64_t v = key | (uint64_t)(1 + g.below((uint32_t)L.C)) << 60;
-    row[L.off_bag + 2 * nmsg] = (uint32_t)v;
-    row[L.off_bag + 2 * nmsg + 1] = (uint32_t)(v >> 32);
+    slot_put(L, row, nmsg, key | (uint64_t)(1 + g.below((uint32_t)L.C)) << 60);
     nmsg++;
   }
   row[L.off_hdr] = (uint32_t)nmsg | (uint32_t)ne << 8;

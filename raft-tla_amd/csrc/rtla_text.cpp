@@ -217,7 +217,8 @@ size_t state_text_into(const Layout& L, const uint32_t* row, char* buf, char* sc
   it.emit(o, "(", " @@ ", ")", "<<>>");
   const int ne = row_nelec(L, row);
   for (int e = 0; e < ne; e++) {
-    const uint32_t* r = row + L.off_elec + e * L.EW;
+    uint32_t r[2 + NMAX];
+    elec_get(L, row, e, r);
     const uint32_t w0 = r[0];
     Out& s = it.scratch;
     it.begin();
@@ -244,6 +245,8 @@ size_t state_text_into(const Layout& L, const uint32_t* row, char* buf, char* sc
     }
   o.s("\n/\\ allLogs = ");
   it.emit(o, "{", ", ", "}", "{}");
+  uint32_t recs[NMAX][3 + NMAX];  // the server records, unpacked
+  for (int i = 0; i < N; i++) srv_get(L, row, i, recs[i]);
   auto per = [&](const char* name, auto fn) {
     o.s("\n/\\ ");
     o.s(name);
@@ -252,7 +255,7 @@ size_t state_text_into(const Layout& L, const uint32_t* row, char* buf, char* sc
       if (i) o.s(" @@ ");
       o.srv((uint32_t)i);
       o.s(" :> ");
-      fn(row + L.off_srv + i * L.SW);
+      fn(recs[i]);
     }
     o.c(')');
   };

@@ -84,6 +84,7 @@ def _load():
         "rtla_probe_bench2": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_double), P(C.c_double),
                                         P(C.c_uint64)]),
         "rtla_row_words": (C.c_int, [P(_Cfg)]),
+        "rtla_row_layout": (C.c_int, [P(_Cfg), P(C.c_int32), C.c_int]),
         "rtla_init_row": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
         "rtla_expand_batch": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, P(C.c_uint32),
                                         P(C.c_uint64), C.c_size_t, P(C.c_size_t)]),
@@ -119,7 +120,7 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
             "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step",
             "rtla_synthetic_generate", "rtla_synthetic_dedup", "rtla_orbit_key", "rtla_permute_row",
-            "rtla_rows_text_hash", "rtla_level_text_hash"]
+            "rtla_rows_text_hash", "rtla_level_text_hash", "rtla_row_layout"]
 
 SYNTH_SEED = 0x5AF72025  # the synthetic microbench's PRNG seed
 
@@ -191,6 +192,18 @@ def _check(st: int, what: str):
 def row_words(cfg: Config) -> int:
     cc = cfg.c()
     return _check(_lib.rtla_row_words(C.byref(cc)), "rtla_row_words")
+
+
+ROW_LAYOUT_KEYS = ("W", "off_hdr", "off_srv", "srv_words", "off_all", "all_words", "off_elec", "elec_words",
+                   "off_bag", "slot_words")
+
+
+def row_layout(cfg: Config) -> dict:
+    """Geometry of the packed row (rtla_model.h make_layout): word offsets and record sizes."""
+    cc = cfg.c()
+    out = (C.c_int32 * len(ROW_LAYOUT_KEYS))()
+    n = _check(_lib.rtla_row_layout(C.byref(cc), out, len(ROW_LAYOUT_KEYS)), "rtla_row_layout")
+    return dict(zip(ROW_LAYOUT_KEYS[:n], list(out)[:n]))
 
 
 def init_row(cfg: Config):

@@ -15,7 +15,6 @@ import pytest
 
 import rtla
 
-OFF_SRV, OFF_HDR = 5, 4  # rtla_model.h make_layout
 
 
 def cfg_of(n):
@@ -27,14 +26,15 @@ def cfg_of(n):
 def look_alike(cfg, row, k):
     """Servers 1..k take server 0's record relabelled into their place (the
     image of record 0 under the transposition (0 i)); the bag is emptied."""
-    n, sw = cfg.n_server, 3 + cfg.n_server
+    n, g = cfg.n_server, rtla.row_layout(cfg)
+    off, sw = g["off_srv"], g["srv_words"]
     out = list(row)
     for i in range(1, k + 1):
         pi = list(range(n))
         pi[0], pi[i] = i, 0
         img = rtla.permute_row(cfg, row, pi)
-        out[OFF_SRV + i * sw:OFF_SRV + (i + 1) * sw] = img[OFF_SRV + i * sw:OFF_SRV + (i + 1) * sw]
-    out[OFF_HDR] &= ~0xFF
+        out[off + i * sw:off + (i + 1) * sw] = img[off + i * sw:off + (i + 1) * sw]
+    out[g["off_hdr"]] &= ~0xFF
     return out
 
 

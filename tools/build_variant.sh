@@ -8,7 +8,8 @@ D=$ROOT/exp/$name; mkdir -p $D
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
 S=$ROOT/raft-tla_amd/csrc
-for u in rtla_kernels rtla_kspec_a rtla_kspec_b rtla_ksym rtla_kgeneric_a rtla_kgeneric_b; do
+for u in rtla_kernels rtla_kwave rtla_kpack rtla_kspec_a rtla_kspec_b rtla_ksym_a rtla_ksym_b rtla_kgeneric_a \
+         rtla_kgeneric_b; do
   $H $F -c -o $D/$u.o $S/$u.hip &
 done
 $H $F -c -o $D/h.o $S/rtla_host.cpp &
