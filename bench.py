@@ -8,13 +8,17 @@ Workloads:
 * ``cfg2`` (default) -- BASELINE.json configs[1] exactly as stated: 3 servers,
   Value = {v1, v2}, currentTerm <= 3, Len(log) <= 2, <= 1 copy per message,
   ElectionSafety + LogMatching, NO in-flight bound.  Its state space grows ~3x
-  per BFS level and does not fit one GPU (nor TLC), so the search runs until
-  device memory is full: a sizing run finds the deepest level whose next level
-  no longer fits (the row arena, the fingerprint set or the row format runs
-  out -- reported, never truncated), then every timed step is a BFS from Init
-  through exactly those complete levels.  value = distinct states found /
-  wall time per step; ``exhausted`` is false and ``levels`` / ``distinct``
-  say how far it got.
+  per BFS level and does not fit one GPU (nor TLC), so a timed step is a BFS
+  from Init through a fixed number of complete levels: the levels the CPU
+  oracle pins (tests/golden/bfs_counts.json: 17 levels, 525,432,784 states,
+  every level's counts and state set checked by the -m gpu suite).
+  ``capacity`` says what the device memory holds beyond them (arena rows,
+  fingerprint-set load, whether the next level's estimated size fits).
+  value = distinct states found / wall time per step; ``exhausted`` is false.
+  Workloads without a pinned depth (configs[3]) run until device memory is
+  full: a sizing run finds the deepest level whose next level no longer fits
+  (reported, never truncated), then every timed step runs exactly those
+  levels.
 * ``cfg1`` -- BASELINE.json configs[0], the bounds of the reference's raft.cfg
   (3 servers, one value, term <= 2, log <= 1, 1 copy), NoTwoLeaders; capped
   the same way.
@@ -62,7 +66,11 @@ SYMMETRIC = {"cfg4"}
 # (SURVEY.md section 8(d)): 3 servers, 2 values, term <= 4, log <= 3, 2 copies
 WORKLOADS["synthetic"] = (3, 2, 4, 3, 2, 0, ES_LM)
 BASELINE_INDEX = {"cfg1": 0, "cfg2": 1, "cfg3": 2, "cfg4": 3, "synthetic": 4}
-CAPPED = {"cfg1", "cfg2", "cfg3", "cfg4"}  # not exhaustible on one GPU: run until HBM is full
+CAPPED = {"cfg1", "cfg2", "cfg3", "cfg4"}  # not exhaustible on one GPU
+# Complete levels of each capped workload that the CPU oracle pins (per-level
+# counts and state-set digests in tests/golden/bfs_counts.json): a timed step
+# runs exactly these (--depth fit: as many as device memory holds instead).
+PINNED_LEVELS = {"cfg1": 23, "cfg2": 17, "cfg3": 14}
 DEFAULT = "cfg2"
 SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run reports it too)
 # Fingerprint-set size (log2 slots) per workload: ~25-30 % load at the size reached.
@@ -224,6 +232,7 @@ class Run:
                                mem_budget=(200 << 30) if args.shards > 1 else 0)
         self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
         self.levels_cap = None   # complete levels a capped search reaches
+        self.pinned = PINNED_LEVELS.get(name) if args.depth == "pinned" else None
         self.stop = None         # what stopped the sizing run
         self.exhausted = False
 
@@ -236,6 +245,7 @@ class Run:
         while st == self.rtla.OK:
             try:
                 st = ck.step()
+                progress("%s sizing: level %d, %d distinct" % (self.name, len(ck.levels), ck.distinct))
             except self.rtla.RtlaError as e:
                 if e.status != -3:  # only capacity may stop a capped search
                     raise
@@ -260,19 +270,29 @@ class Run:
         return ck.levels
 
 
+def progress(msg):
+    """A progress line on stderr (long runs keep writing: a silent GPU job is taken to be hung)."""
+    if dist_env()[0] == 0:
+        print("bench.py: " + msg, file=sys.stderr, flush=True)
+
+
 def timed(run, steps, warmup, world, barrier, cap_levels=0):
     if run.capped and cap_levels:
         run.levels_cap, run.exhausted, run.stop = cap_levels, False, "--cap-levels %d" % cap_levels
+    elif run.capped and run.pinned:
+        run.levels_cap, run.exhausted, run.stop = run.pinned, False, "oracle-pinned depth (%d levels)" % run.pinned
     elif run.capped:
         run.size()
-    for _ in range(warmup):
+    for w in range(warmup):
         run.one()
+        progress("%s warmup %d/%d" % (run.name, w + 1, warmup))
     barrier()
     t0 = time.perf_counter()
     levels = None
     for _ in range(steps):
         levels = run.one()
     t1 = time.perf_counter()
+    progress("%s timed %d steps: %.1f ms/step" % (run.name, steps, (t1 - t0) / steps * 1e3))
     barrier()
     return max_over_ranks(t1 - t0, world) / steps, levels
 
@@ -312,6 +332,20 @@ def roofline(levels, world, workload):
                           # SURVEY.md 8(d)'s probe term: probes / (t * the calibrated random 8-B CAS rate)
                           "frac_vs_cas_rate": P / world / (ems / 1e3) / CAS_PER_S},
     }
+
+
+def capacity(levels, info, fpl):
+    """What device memory holds beyond the timed levels: the frontier arena
+    (current + next level share it), the fingerprint set's load, and whether
+    the next level -- estimated from the last level's growth -- would fit."""
+    rows = info.get("frontier_cap") or 0
+    last, prev = levels[-1].new, levels[-2].new if len(levels) > 1 else 1
+    est_next = int(last * last / max(1, prev))
+    distinct = sum(lv.new for lv in levels)
+    return {"arena_rows": rows, "row_bytes": levels[0].row_bytes, "fpset_slots_log2": fpl,
+            "fpset_load": distinct / float(1 << fpl), "last_level": last, "next_level_estimate": est_next,
+            "next_level_fits_arena": rows >= ((last + 63) // 64) * 64 + est_next,
+            "fpset_load_after_next": (distinct + est_next) / float(1 << fpl)}
 
 
 def synthetic(run, args, rank, world, barrier):
@@ -369,6 +403,8 @@ def main():
     ap.add_argument("--levels", action="store_true", help="print the per-level tables to stderr")
     ap.add_argument("--synth-states", type=int, default=SYNTH_STATES,
                     help="synthetic workload: input states per GPU")
+    ap.add_argument("--depth", choices=("pinned", "fit"), default="pinned",
+                    help="capped workloads: the oracle-pinned levels (default), or as many as device memory holds")
     ap.add_argument("--cap-levels", type=int, default=0,
                     help="capped workloads: run exactly this many complete levels and skip the sizing run "
                          "(profiling; a level that does not fit is still an error)")
@@ -472,6 +508,8 @@ def main():
     }
     if run.capped:
         config["stopped_by"] = run.stop
+        config["oracle_pinned"] = bool(run.pinned) and not args.cap_levels
+        config["capacity"] = capacity(levels, info, run.fpl)
     out = {
         "metric": "distinct states/sec (whole node) + wall time to exhaust, 3-server Raft",
         "value": distinct / per_step,

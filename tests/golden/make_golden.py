@@ -61,9 +61,10 @@ PREFIXES = {
 # SYMMETRY prefixes (orbit counts per level; no text hashes: the orbit
 # representatives kept differ between implementations).  N = 4 and BASELINE
 # configs[3] (N = 5) as stated.
+# name: (N, V, T, L, C, M, invariants, max_distinct, max_levels)
 SYM_PREFIXES = {
-    "n4_v1_t2_l1_m1_sym_prefix": (4, 1, 2, 1, 1, 1, (NTL,), 3_000_000),
-    "n5_v1_t3_l2_c1_sym_prefix": (5, 1, 3, 2, 1, 0, (), 3_000_000),
+    "n4_v1_t2_l1_m1_sym_prefix": (4, 1, 2, 1, 1, 1, (NTL,), 3_000_000, 0),
+    "n5_v1_t3_l2_c1_sym_prefix": (5, 1, 3, 2, 1, 0, (), 3_000_000, 0),
 }
 
 
@@ -127,10 +128,11 @@ def main():
         print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
         with open(path, "w") as f:  # each prefix is long: keep what is done
             json.dump(out, f, indent=1, sort_keys=True)
-    for name, (n, v, t, l, c, m, inv, cap) in SYM_PREFIXES.items():
+    for name, (n, v, t, l, c, m, inv, cap, depth) in SYM_PREFIXES.items():
         if not big or (only and name not in only):
             continue
-        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap, symmetry=True)
+        cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap, symmetry=True, max_levels=depth)
+        cfg.verbose = 1
         r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8)
         assert r["rc"] in (0, -4), (name, r["rc"])
         out[name] = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
