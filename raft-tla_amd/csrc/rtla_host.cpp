@@ -16,7 +16,13 @@
 //                             materialise + invariants).
 //   world == N (one process per GPU, RCCL over xGMI): one shard per rank.
 //   world == 1, shards == S : S shards on one GPU, exchanging by device copies
-//                             -- the multi-GPU protocol exercised on one device.
+//                             -- the multi-GPU protocol exercised on one device;
+//                             with RTLA_TRANSPORT=rccl the same exchange runs
+//                             through a one-rank RCCL communicator instead
+//                             (every ncclSend/ncclRecv to self, the count
+//                             all-gathers, the level all-reduces, the trace
+//                             broadcasts): the RCCL call sites of the
+//                             multi-GPU path execute on a one-GPU box.
 //
 // Multi-shard level (per chunk of the frontier, all shards in lock-step):
 //   1. k_expand: successors owned locally are probed/inserted/materialised at
@@ -125,6 +131,7 @@ struct rtla_ctx {
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   ShmComm* shm = nullptr;  // RTLA_TRANSPORT=shm instead of RCCL
+  bool rccl_local = false; // world 1, S shards, RTLA_TRANSPORT=rccl: the exchange goes through `comm` (1 rank)
   int tlog2 = 0;
   uint64_t front_cap = 0, box_cap = 0, chunk = 0, rows_cap = 0;
   uint64_t* red = nullptr;  // device scratch for all-reduces
@@ -771,6 +778,16 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
       memcpy(&id, comm_id, sizeof id);
       if (ncclCommInitRank(&x->comm, world, id, rank) != ncclSuccess) { rtla_close(x); return RTLA_E_COMM; }
     }
+  } else if (x->nshard > 1) {
+    const char* tr = getenv("RTLA_TRANSPORT");
+    if (tr && !strcmp(tr, "rccl")) {  // virtual shards exchanging through a one-rank RCCL communicator
+      ncclUniqueId id;
+      if (ncclGetUniqueId(&id) != ncclSuccess || ncclCommInitRank(&x->comm, 1, id, 0) != ncclSuccess) {
+        rtla_close(x);
+        return RTLA_E_COMM;
+      }
+      x->rccl_local = true;
+    }
   }
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
@@ -830,9 +847,11 @@ extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
   HIPCHK(hipGetDeviceProperties(&p, x->device));
   snprintf(buf, cap,
            "{\"device\": \"%s\", \"arch\": \"%s\", \"cus\": %d, \"rank\": %d, \"world\": %d, \"shards\": %d, "
-           "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu}",
+           "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu, "
+           "\"transport\": \"%s\"}",
            p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
-           (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk);
+           (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk,
+           x->shm ? "shm" : x->comm ? (x->rccl_local ? "rccl-local" : "rccl") : "device");
   return RTLA_OK;
 }
 
@@ -842,7 +861,7 @@ static double now_s() {
 
 // Sum of n1 u64 and max of n2 u64 over all ranks (one synchronisation); host in/out.
 static int allreduce2_u64(rtla_ctx* x, uint64_t* sum, int n1, uint64_t* mx, int n2) {
-  if (x->world == 1) return RTLA_OK;
+  if (x->world == 1 && !x->rccl_local) return RTLA_OK;
   HIPCHK(hipMemcpyAsync(x->red, sum, 8 * n1, hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipMemcpyAsync(x->red + 32, mx, 8 * n2, hipMemcpyHostToDevice, x->stream));
   if (!x->shm) NCCLCHK(ncclGroupStart());
@@ -857,7 +876,7 @@ static int allreduce2_u64(rtla_ctx* x, uint64_t* sum, int n1, uint64_t* mx, int 
 
 // Sum (op 0) or max (op 1) of n u64 over all ranks; host in/out.
 static int allreduce_u64(rtla_ctx* x, uint64_t* v, int n, int op) {
-  if (x->world == 1) return RTLA_OK;
+  if (x->world == 1 && !x->rccl_local) return RTLA_OK;
   HIPCHK(hipMemcpyAsync(x->red, v, 8 * n, hipMemcpyHostToDevice, x->stream));
   if (int rc = comm_allreduce(x, x->red, n, op)) return rc;
   HIPCHK(hipMemcpyAsync(v, x->red, 8 * n, hipMemcpyDeviceToHost, x->stream));
@@ -1082,12 +1101,38 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
 // fingerprint and answer transfers; (2) after the owners' inserts, to learn
 // every (owner, sender) winner count, which sizes the row transfers.
 
+// One exchange between the shards of this process: device copies, or (rccl_local)
+// one RCCL group of ncclSend/ncclRecv pairs to rank 0 -- this process -- issued
+// in the same order, so the i-th send feeds the i-th receive.
+struct Local {
+  rtla_ctx* x;
+  std::vector<Msg> sends, recvs;
+  explicit Local(rtla_ctx* x_) : x(x_) {}
+  int move(void* dst, const void* src, size_t bytes) {
+    if (!x->rccl_local) {
+      HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, x->stream));
+      return RTLA_OK;
+    }
+    sends.push_back({const_cast<void*>(src), bytes, 0});
+    recvs.push_back({dst, bytes, 0});
+    return RTLA_OK;
+  }
+  int flush() { return sends.empty() ? RTLA_OK : comm_exchange(x, sends, recvs); }
+};
+
 // (1) h_out[p] = records this shard queued for owner p, h_in[p] = records
 // owner-shard receives from p; in_count on the device.
 static int gather_counts(rtla_ctx* x) {
   const int G = x->nshard;
   if (x->world == 1) {
-    for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.h_out.data(), s.out_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+    for (auto& s : x->sh) {
+      if (x->rccl_local) {  // (one rank: all_count[0, G) = out_count)
+        if (int rc = comm_allgather(x, s.out_count, s.all_count, G)) return rc;
+        HIPCHK(hipMemcpyAsync(s.h_out.data(), s.all_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+      } else {
+        HIPCHK(hipMemcpyAsync(s.h_out.data(), s.out_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+      }
+    }
     HIPCHK(hipStreamSynchronize(x->stream));
     for (auto& dst : x->sh)
       for (auto& src : x->sh) dst.h_in[src.id] = src.h_out[dst.id];
@@ -1118,14 +1163,16 @@ static int move_fps(rtla_ctx* x) {
   const int G = x->nshard;
   const uint64_t cap = x->box_cap;
   if (x->world == 1) {
+    Local lc(x);
     for (auto& dst : x->sh)
       for (auto& src : x->sh) {
         const uint64_t n = src.h_out[dst.id];
         if (n)
-          HIPCHK(hipMemcpyAsync(dst.recv_fp + 2 * (uint64_t)src.id * cap, src.send_fp + 2 * (uint64_t)dst.id * cap,
-                                16 * n, hipMemcpyDeviceToDevice, x->stream));
+          if (int rc = lc.move(dst.recv_fp + 2 * (uint64_t)src.id * cap, src.send_fp + 2 * (uint64_t)dst.id * cap,
+                               16 * n))
+            return rc;
       }
-    return RTLA_OK;
+    return lc.flush();
   }
   Shard& s = x->sh[0];
   std::vector<Msg> sends, recvs;
@@ -1144,14 +1191,23 @@ static int move_answers(rtla_ctx* x) {
   const int G = x->nshard;
   const uint64_t cap = x->box_cap;
   if (x->world == 1) {
-    for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.new_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+    for (auto& s : x->sh) {
+      if (x->rccl_local) {
+        if (int rc = comm_allgather(x, s.new_count, s.all_new, G)) return rc;
+        HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.all_new, 8 * G, hipMemcpyDeviceToHost, x->stream));
+      } else {
+        HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.new_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+      }
+    }
+    Local lc(x);
     for (auto& src : x->sh)
       for (auto& dst : x->sh) {
         const uint64_t n = src.h_out[dst.id];
         if (n)
-          HIPCHK(hipMemcpyAsync(src.send_ans + (uint64_t)dst.id * cap, dst.recv_ans + (uint64_t)src.id * cap, 4 * n,
-                                hipMemcpyDeviceToDevice, x->stream));
+          if (int rc = lc.move(src.send_ans + (uint64_t)dst.id * cap, dst.recv_ans + (uint64_t)src.id * cap, 4 * n))
+            return rc;
       }
+    if (int rc = lc.flush()) return rc;
     HIPCHK(hipStreamSynchronize(x->stream));
     for (auto& src : x->sh)
       for (auto& dst : x->sh) src.h_new_out[dst.id] = dst.h_new_in[src.id];
@@ -1196,14 +1252,16 @@ static int move_rows(rtla_ctx* x, uint64_t lo) {
   auto part = [&](uint64_t n) { return n > lo ? std::min<uint64_t>(n - lo, rc) : 0; };
   for (auto& s : x->sh) HIPCHK(launch_part_counts(s.new_count, G, lo, rc, s.rows_in, s.rows_base, s.ctr, x->stream));
   if (x->world == 1) {
+    Local lc(x);
     for (auto& dst : x->sh)
       for (auto& src : x->sh) {
         const uint64_t n = part(src.h_new_out[dst.id]);
         if (n)
-          HIPCHK(hipMemcpyAsync(dst.recv_rows + (uint64_t)src.id * rc * RW, src.send_rows + (uint64_t)dst.id * rc * RW,
-                                4 * n * RW, hipMemcpyDeviceToDevice, x->stream));
+          if (int r = lc.move(dst.recv_rows + (uint64_t)src.id * rc * RW, src.send_rows + (uint64_t)dst.id * rc * RW,
+                              4 * n * RW))
+            return r;
       }
-    return RTLA_OK;
+    return lc.flush();
   }
   Shard& s = x->sh[0];
   std::vector<Msg> sends, recvs;
@@ -1516,8 +1574,13 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
   uint64_t shard = start[1], g = start[2];
   for (int guard = 0; guard < (1 << 20); guard++) {
     uint64_t p = 0;
-    if (x->world == 1) {
+    if (x->world == 1 && !x->rccl_local) {
       HIPCHK(hipMemcpy(&p, x->sh[shard].parents + g, 8, hipMemcpyDeviceToHost));
+    } else if (x->world == 1) {  // the record travels through the one-rank communicator too
+      HIPCHK(hipMemcpyAsync(x->red, x->sh[shard].parents + g, 8, hipMemcpyDeviceToDevice, x->stream));
+      if (int rc2 = comm_bcast(x, x->red, 1, 0)) return rc2;
+      HIPCHK(hipMemcpyAsync(&p, x->red, 8, hipMemcpyDeviceToHost, x->stream));
+      HIPCHK(hipStreamSynchronize(x->stream));
     } else {
       if ((int)shard == x->rank) HIPCHK(hipMemcpyAsync(x->red, x->sh[0].parents + g, 8, hipMemcpyDeviceToDevice, x->stream));
       if (int rc2 = comm_bcast(x, x->red, 1, (int)shard)) return rc2;

@@ -266,6 +266,57 @@ def test_virtual_shards_match_golden(name, shards):
     assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
 
 
+@pytest.mark.parametrize("shards", [2, 3, 8])
+@pytest.mark.parametrize("name", ["n2_v2_t3_l2_m1", "n3_v1_t2_l1_m1", "n2_v1_t2_l1_m1_sym"])
+def test_virtual_shards_over_rccl_match_golden(monkeypatch, name, shards):
+    """The virtual-shard exchange through a one-rank RCCL communicator
+    (RTLA_TRANSPORT=rccl): every fingerprint / answer / row transfer is an
+    ncclSend/ncclRecv pair to self inside one group, the count and winner
+    gathers are ncclAllGather, the level reductions ncclAllReduce -- the RCCL
+    call sites of the multi-GPU path, executed on this GPU.  Golden per-level
+    counts, as with device copies."""
+    monkeypatch.setenv("RTLA_TRANSPORT", "rccl")
+    g = GOLD[name]
+    kw = small_kw(g)
+    kw["mem_budget"] *= shards
+    with rtla.Checker(cfg_of(g, shards=shards, chunk=512, **kw)) as ck:
+        assert json.loads(ck.device_info())["transport"] == "rccl-local"
+        st = ck.init()
+        while st == rtla.OK:
+            st = ck.step()
+        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
+        assert ck.distinct == g["distinct"]
+
+
+def test_virtual_shards_over_rccl_trace_and_contents(monkeypatch):
+    """Through the one-rank RCCL communicator: level contents (text digests,
+    whose cross-shard sum is an ncclAllReduce) and a counterexample trace whose
+    parent records travel by ncclBroadcast."""
+    monkeypatch.setenv("RTLA_TRANSPORT", "rccl")
+    g = GOLD["n2_v2_t3_l2_m1"]
+    kw = small_kw(g)
+    kw["mem_budget"] *= 4
+    got = []
+    with rtla.Checker(cfg_of(g, shards=4, chunk=1000, **kw)) as ck:
+        st = ck.init()
+        while True:
+            got.append("%016x" % ck.level_text_hash())
+            if st != rtla.OK:
+                break
+            st = ck.step()
+    assert got[:len(g["level_text_hash"])] == g["level_text_hash"]
+    g = GOLD["n3_v1_t3_l1_m1_ntl"]
+    kw = small_kw(g)
+    kw["mem_budget"] *= 3
+    res = rtla.check(cfg_of(g, shards=3, **kw))
+    assert res.violation == "NoTwoLeaders" and len(res.trace) == g["depth"]
+    walk = raft_cpu.Walk(raft_cpu.cfg_of(3, 1, 3, 1, 1, 1, ("NoTwoLeaders",)))
+    for label, text in res.trace[1:]:
+        assert text in [t for _, t in walk.successors()], label
+        walk.goto(text)
+    assert walk.invariants() & 1
+
+
 def test_virtual_shards_level_contents():
     g = GOLD["n2_v2_t3_l2_m1"]
     kw = small_kw(g)
@@ -604,25 +655,30 @@ def test_synthetic_states_successors_match_value_oracle():
 
 def test_synthetic_step_dedup_counts():
     """rtla_synthetic_step (the dedup-only level kernel over device-generated
-    states) against a host recount from rtla_expand_batch over the same rows:
-    generated successors, fingerprint-set probes (in-model successors that are
-    not their parent) and distinct new fingerprints, across two batches that
-    share the fingerprint set."""
+    states) against counts from the VALUE ORACLE over the same rows (each
+    input parsed from its text, raft_values.next_states): generated
+    successors, fingerprint-set probes (in-model successors that differ from
+    their parent) and distinct new states, across two batches that share the
+    fingerprint set."""
+    import tla_text
     cfg = rtla.Config(**SYNTH, fpset_log2=22, mem_budget=1 << 30)
-    n, pool = 2500, 400
+    vc = rv.Cfg(3, 2, 4, 3, 2, ("ElectionSafety", "LogMatching"), 0)
+    n, pool = 320, 60
     rows = rtla.random_rows(cfg, 0, 2 * n, pool=pool)
-    fps = set()
+    seen = set()
     expect = []
     for b in range(2):
         gen = probes = 0
-        before = len(fps)
-        part = rows[b * n:(b + 1) * n]
-        for k, inst, sub, im, r in rtla.expand_batch(cfg, part):
-            gen += 1
-            if im and r[:4] != part[k][:4]:
-                probes += 1
-                fps.add(tuple(r[:4]))
-        expect.append((gen, probes, len(fps) - before))
+        before = len(seen)
+        for r in rows[b * n:(b + 1) * n]:
+            text = rtla.state_text(cfg, r)
+            for _, t in rv.next_states(vc, tla_text.parse_state(vc, text)):
+                gen += 1
+                tt = rv.state_text(vc, t)
+                if rv.in_model(vc, t) and tt != text:
+                    probes += 1
+                    seen.add(tt)
+        expect.append((gen, probes, len(seen) - before))
     with rtla.Checker(cfg) as ck:
         got = [ck.synthetic_step(b * n, n, pool) for b in range(2)]
     assert [(lv.generated, lv.probes, lv.new) for lv in got] == expect

@@ -17,7 +17,8 @@ step() {
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM"
 SQ2="SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM"
 for W in ${WORKLOADS:-cfg2 raft3_v2_t2_l2_m2}; do
-  CAP=""; [ "$W" = cfg2 ] && CAP="--cap-levels 17"
+  # the benched depth without a sizing run inside the profile (cfg4: no oracle-pinned depth)
+  CAP=""; [ "$W" = cfg2 ] && CAP="--cap-levels 17"; [ "$W" = cfg4 ] && CAP="--cap-levels 15"
   B="python bench.py --steps 1 --warmup 0 --no-cpu --no-secondary --workload $W $CAP"
   step $W.kt 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$W/kt" -o kt -- $B
   step $W.fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/$W/p1" -o p -- $B
