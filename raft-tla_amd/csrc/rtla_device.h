@@ -95,6 +95,7 @@ struct DevCounters {
   unsigned long long viol_child;
   unsigned long long group_next;  // k_expand_compact's work queue (zeroed before each launch)
   unsigned long long stamp[8];    // RTLA_STAMPS builds: cycles per level-kernel phase, summed over waves
+  unsigned long long cas;         // RTLA_COUNT_CAS builds: pipelined fingerprint-set CAS issued by the level kernel
   // buffer capacities (rows of the current / next frontier, parent records), for RTLA_CHECKED builds
   unsigned long long cap_cur, cap_next, cap_parents;
   unsigned long long cover[2 * COVER_CODES];  // [0,C): generated, [C,2C): distinct

@@ -340,12 +340,12 @@ constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a 
 // per-state fingerprint with allLogs' applied (GROUP FPs) | SYMMETRY: the
 // fingerprint of each state's allLogs' (GROUP FPs) | per-owner (base, used)
 // of the open outbox chunk | pending new states (NEWCAP u16 entries) |
-// GROUP rows | allLogs' words of each state | pair ring.
+// GROUP rows | allLogs' words of each state | pair ring | SYMMETRY: key ring.
 // (The outbox state exists only in the MULTI kernels: one shard's tile then
 // stays small enough for 12 one-wave blocks per CU on configs[1]'s 372-byte rows.)
 __host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym, bool multi) {
-  return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW + RING / 2 +
-          3) & ~3;
+  return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW +
+          RING / 2 * (sym ? 2 : 1) + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -418,6 +418,12 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #ifndef RTLA_SYM_WAVES_PER_EU
 #define RTLA_SYM_WAVES_PER_EU 2      // SYMMETRY: the full Delta and the orbit-key loop stay in VGPRs
 #endif
+#ifndef RTLA_MULTI_ASYNC
+#define RTLA_MULTI_ASYNC 1  // multi-shard kernels pipeline their CAS too
+#endif
+#ifndef RTLA_SYM_SPLIT
+#define RTLA_SYM_SPLIT 1  // SYMMETRY: orbit keys in a pass of their own (key_chunk), not inside the evaluation
+#endif
 // The layout the kernel runs on: the run-time argument, or (LC.N != 0) the
 // configuration compiled in as a template parameter, whose fields the
 // compiler then folds into every offset, bound and loop of the model code.
@@ -464,6 +470,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
                  unsigned long long next_base, unsigned long long next_cap, unsigned long long* table,
                  unsigned long long* sent, int tlog2, DevCounters* ctr, ShardBox box, int xflags) {
   const Layout& L = pick_layout<LC>(Lrt);
+  constexpr bool KSPLIT = SYM && RTLA_SYM_SPLIT;
   const int me = box.me;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[2 * COVER_CODES];
@@ -479,6 +486,10 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   uint32_t* pall = rows + GROUP * W;  // allLogs' words of state lane l: pall[l + w * GROUP]
   const StridedWords<GROUP> pall_mine{pall + (lane & (GROUP - 1))};
   uint16_t* ring = reinterpret_cast<uint16_t*>(pall + GROUP * AW);
+  // SYMMETRY: successors that need an orbit key (in-model, not the parent),
+  // queued by the evaluation pass and keyed 64 at a time (key_chunk)
+  uint16_t* kring = ring + RING;
+  int kpos = 0, kdone = 0;
   if (MULTI) {
     if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
@@ -490,6 +501,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   __syncthreads();
 
   unsigned my_gen = 0, my_probe = 0;
+#ifdef RTLA_COUNT_CAS
+  unsigned my_cas = 0;
+#endif
   const int ninst = L.fam[F_COUNT];
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
   RTLA_STAMP_DECL
@@ -501,16 +515,19 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   unsigned long long pold = 0;
   FP pf{0, 0};       // its fingerprint (home slot and owner derive from it)
   uint32_t pinfo = 0;  // its state lane << 16 | action instance
-  // Single shard: a probe whose home-slot load did not show its key issues
-  // ONE CAS -- at the home slot if it read empty, else at the next slot
-  // (linear probing; slots only ever go 0 -> key) -- together with the next
-  // chunk's loads, and that CAS is resolved a chunk later: neither the
-  // insert nor the first collision step waits for a round trip.
-  const bool async_cas = !MULTI && !(xflags & XF_CAS_ONLY);
+  // A probe whose home-slot load did not show its key issues ONE CAS -- at
+  // the home slot if it read empty, else at the next slot (linear probing;
+  // slots only ever go 0 -> key) -- together with the next chunk's loads,
+  // and that CAS is resolved a chunk later: neither the insert nor the first
+  // collision step waits for a round trip.  (MULTI: in the set or, for a
+  // successor another shard owns, in the sent cache.)
+  const bool async_cas = (!MULTI || RTLA_MULTI_ASYNC) && !(xflags & XF_CAS_ONLY);
   bool cpend = false;    // CAS set up by resolve(), issued by issue_cas()
   bool cflight = false;  // CAS in flight (result in cold)
   unsigned long long cold = 0, ckey = 0, cidx = 0;
   uint32_t cinfo = 0;
+  FP cf{0, 0};     // MULTI: the CAS'd successor's fingerprint (its outbox record) ...
+  int cowner = me; // ... and owner
   // New states found so far whose rows are not built yet: newl[head, tail)
   // (mod NEWCAP) holds (state lane, instance); their parents are rows of the
   // current group (uniform counters).  They are built when the group's probes
@@ -618,24 +635,31 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     head = tail;
   };
   auto issue_cas = [&]() {
-    if (cpend) cold = atomicCAS(&table[cidx], 0ull, ckey);
+#ifdef RTLA_COUNT_CAS
+    if (cpend) my_cas++;
+#endif
+    if (cpend) cold = atomicCAS(&((MULTI && cowner != me) ? sent : table)[cidx], 0ull, ckey);
     cflight = cpend;
     cpend = false;
   };
   auto resolve = [&]() {
     bool isnew = false;
-    uint32_t ninfo = pinfo;  // the state isnew refers to
+    // the state isnew refers to: its (tile row, instance), fingerprint and owner
+    uint32_t ninfo = pinfo;
     const int powner = MULTI ? fp_owner(pf, box.nshard) : me;
-    const unsigned long long prec =
-        (unsigned long long)me << 56 | (cur_base + s0 + (pinfo >> 16)) << 16 | (unsigned long long)(pinfo & 0xffffu);
+    FP nf = pf;
+    int nowner_r = powner;
     if (xflags & XF_ALL_SUCCESSORS) {  // every enabled successor is output (no seen set)
       isnew = pend;
     } else if (async_cas) {
       if (cflight) {  // the CAS issued one chunk ago
         if (cold == 0ull) isnew = true;
-        else if (cold != ckey) isnew = fpset_resolve(table, tlog2, ckey, cidx, cold, ctr);  // rare: keep probing
+        else if (cold != ckey)  // rare: keep probing
+          isnew = fpset_resolve((MULTI && cowner != me) ? sent : table, tlog2, ckey, cidx, cold, ctr);
       }
       ninfo = cinfo;
+      nf = cf;
+      nowner_r = cowner;
       cflight = false;
       if (pend) {  // this chunk's load -> seen, or a CAS for the next issue
         const unsigned long long key = pf.b | 1ull, idx = pf.a >> (64 - tlog2);
@@ -643,6 +667,10 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           cidx = pold == 0ull ? idx : ((idx + 1ull) & ((1ull << tlog2) - 1ull));
           ckey = key;
           cinfo = pinfo;
+          if (MULTI) {
+            cf = pf;
+            cowner = powner;
+          }
           cpend = true;
         }
       }
@@ -654,6 +682,10 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
                                      : fpset_resolve_loaded(t, tlog2, pf.b | 1ull, pidx, pold, ctr, to_sent);
     }
     if (MULTI) {  // records for other owners: one outbox reservation per (wave, owner)
+      const int powner = nowner_r;
+      const FP pf = nf;
+      const unsigned long long prec =
+          (unsigned long long)me << 56 | (cur_base + s0 + (ninfo >> 16)) << 16 | (unsigned long long)(ninfo & 0xffffu);
       const bool rem = isnew && powner != me;
       isnew = isnew && powner == me;
       unsigned long long om = wave_or_u64(rem ? 1ull << powner : 0ull);
@@ -708,40 +740,44 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   FP ncf{0, 0};
   int nowner = me;
   uint32_t ninfo_new = 0;
+  // compute_delta over a chunk, specialised for its family when the whole
+  // chunk holds one (D = DeltaFpT for the probe pass, DeltaT for orbit keys)
+  auto chunk_delta = [&](bool active, const uint32_t* prow, int inst, auto& d) {
+    const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
+    const bool one_family = __ballot(active && inst_family(L, inst) != f0) == 0ull;
+    if (!one_family || (xflags & XF_GENERIC_DELTA)) {
+      if (active) compute_delta<NS>(L, prow, inst, d);
+    } else if (active) {
+      switch (f0) {  // one family in the whole chunk: its code only
+        case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
+        case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
+        case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
+        case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
+        case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
+        case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
+        case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
+        case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
+        case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
+        default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
+      }
+    }
+  };
   auto eval_chunk = [&](int done, int cnt) {
     const bool active = lane < cnt;
     const int e = active ? ring[(done + lane) & (RING - 1)] : 0;
     const int sl = e >> 8, inst = e & 255;
     const uint32_t* prow = rows + sl * W;
     const FP qfp = pfpl[sl];
-    std::conditional_t<SYM, DeltaT<NS>, DeltaFpT<NS>> d;
+    std::conditional_t<SYM && !KSPLIT, DeltaT<NS>, DeltaFpT<NS>> d;
     d.enabled = 0;
-    if (!(xflags & XF_NO_DELTA)) {
-      const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
-      const bool one_family = __ballot(active && inst_family(L, inst) != f0) == 0ull;
-      if (!one_family || (xflags & XF_GENERIC_DELTA)) {
-        if (active) compute_delta<NS>(L, prow, inst, d);
-      } else if (active) {
-        switch (f0) {  // one family in the whole chunk: its code only
-          case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
-          case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
-          case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
-          case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
-          case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
-          case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
-          case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
-          case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
-          case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
-          default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
-        }
-      }
-    }
+    if (!(xflags & XF_NO_DELTA)) chunk_delta(active, prow, inst, d);
     bool en = d.enabled != 0;
     if (en && d.err) {
       set_flag(ctr, d.err == 1 ? FLAG_SPEC_ERROR : FLAG_ROW_OVERFLOW);
       en = false;
     }
     my_gen += en ? 1u : 0u;
+    bool kq = false;
     nprobe = false;
     nidx = 0;
     ncf = FP{0, 0};
@@ -751,20 +787,29 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       nprobe = true;  // "probe" = output it: issue_probe skips the load, resolve takes it as new
     } else if (en && d.in_model) {
       FP cfp;
-      if constexpr (SYM) cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
+      if constexpr (SYM && !KSPLIT) cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
       else
         cfp = (xflags & XF_NO_HASH) ? FP{qfp.a + d.rec[0] + (uint64_t)d.fmsg.a, qfp.b + d.rec[1]}
                                     : fp_add(qfp, delta_fp<NS>(L, prow, d));
       const FP qfp0 = row_fp(prow);
       if (cfp.a != qfp0.a || cfp.b != qfp0.b) {  // successor == parent: already in the set
-        // seen-set key: the fingerprint, or under SYMMETRY the orbit key
-        FP key = cfp;
-        if constexpr (SYM) key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
-        nprobe = !(xflags & XF_NO_PROBE);
-        ncf = key;
-        nidx = key.a >> (64 - tlog2);
-        nowner = MULTI ? fp_owner(key, box.nshard) : me;
+        if constexpr (KSPLIT) {
+          kq = true;  // its seen-set key is the orbit key: queued for key_chunk
+        } else {
+          // seen-set key: the fingerprint, or (SYMMETRY, not split) the orbit key
+          FP key = cfp;
+          if constexpr (SYM) key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
+          nprobe = !(xflags & XF_NO_PROBE);
+          ncf = key;
+          nidx = key.a >> (64 - tlog2);
+          nowner = MULTI ? fp_owner(key, box.nshard) : me;
+        }
       }
+    }
+    if constexpr (KSPLIT) {
+      const unsigned long long km = __ballot(kq);
+      if (kq) kring[(kpos + __popcll(km & lanes_below)) & (RING - 1)] = (uint16_t)(sl << 8 | inst);
+      kpos += __popcll(km);
     }
     if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
       const int code = en ? cover_code(L, inst, d.sub) : -1;
@@ -787,6 +832,29 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       ctr->viol_inst = inst;
       ctr->viol_in_model = 0;
       ctr->viol_child = ~0ull;
+    }
+  };
+  // SYMMETRY: the orbit keys of kring[kd, kd + kc), one per lane: the full
+  // Delta (the probe pass only folded it into a hash), then
+  // successor_orbit_key; the key goes through the probe pipeline.  Kept
+  // apart from the evaluation so that neither pass holds the other's
+  // registers.
+  auto key_chunk = [&](int kd, int kc) {
+    const bool active = lane < kc;
+    const int e = active ? kring[(kd + lane) & (RING - 1)] : 0;
+    const int sl = e >> 8, inst = e & 255;
+    const uint32_t* prow = rows + sl * W;
+    DeltaT<NS> d;
+    d.enabled = 0;
+    if (active) compute_delta<NS>(L, prow, inst, d);  // (generic: the per-family switch costs spills here)
+    nprobe = false;
+    ninfo_new = (uint32_t)sl << 16 | (uint32_t)inst;
+    if (active && d.enabled) {
+      const FP key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
+      nprobe = !(xflags & XF_NO_PROBE);
+      ncf = key;
+      nidx = key.a >> (64 - tlog2);
+      nowner = MULTI ? fp_owner(key, box.nshard) : me;
     }
   };
   auto issue_probe = [&]() {
@@ -890,10 +958,16 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         STAMP(1);  // pair ring
         eval_chunk(done, cnt);
         STAMP(2);  // successor deltas, fingerprints, coverage, out-of-model invariants
-        resolve();  // the previous chunk's probes, after this chunk's arithmetic
-        STAMP(3);
-        issue_probe();
-        STAMP(4);  // probe issue
+        if (!KSPLIT || (xflags & XF_ALL_SUCCESSORS) || kpos - kdone >= 64) {
+          if (KSPLIT && kpos - kdone >= 64) {  // 64 orbit keys are queued: key them (they feed the probe pipeline)
+            key_chunk(kdone, 64);
+            kdone += 64;
+          }
+          resolve();  // the previous chunk's probes, after this chunk's arithmetic
+          STAMP(3);
+          issue_probe();
+          STAMP(4);  // probe issue
+        }
         if (tail - head > NEWFLUSH) {  // rare (early levels): drain the probes, build the rows so far
           drain();
           build_all();
@@ -912,6 +986,12 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     // waits for them before.  (an asm-issued load's register was
     // invisible to the compiler.)
     uint32_t pfa = 0, pfb = 0;
+    if (KSPLIT && kpos > kdone) {  // the group's last orbit keys
+      key_chunk(kdone, kpos - kdone);
+      resolve();
+      issue_probe();
+      kdone = kpos;
+    }
     if (gnn < ngroups) {
       const unsigned long long sn = s_begin + gnn * GROUP;
       const int lines = ((int)min<unsigned long long>((unsigned long long)GROUP, s_end - sn) * W + 31) / 32;
@@ -940,6 +1020,10 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   if (lane == 0 && my_gen) atomicAdd(&ctr->generated, (unsigned long long)my_gen);
   if (lane == 0 && my_probe) atomicAdd(&ctr->probes, (unsigned long long)my_probe);
   if (lane == 0 && dedup_new) atomicAdd(&ctr->next_count, dedup_new);
+#ifdef RTLA_COUNT_CAS
+  for (int off = 32; off > 0; off >>= 1) my_cas += __shfl_down(my_cas, off);
+  if (lane == 0 && my_cas) atomicAdd(&ctr->cas, (unsigned long long)my_cas);
+#endif
   STAMP(7);
   RTLA_STAMP_FLUSH(ctr, lane)
   __syncthreads();

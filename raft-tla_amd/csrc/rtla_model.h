@@ -1408,6 +1408,67 @@ RTLA_HD FP orbit_key_finish(FP m) {
 //   elec_of(e, out) election record e < nelec (2 + NS words)
 //   afp             fingerprint of allLogs (permutation-free)
 // `perms` (optional) receives |C(s)|.
+// Permutations packed 3 bits per server (pim: pi[j] at bits 3j, invm: its
+// inverse), so a loop over servers indexes them with shifts: the orbit-key
+// loops below stay rolled (one record live at a time) instead of unrolling
+// into N records' worth of registers.  Same values as the array forms above.
+template <int NS>
+RTLA_HD uint32_t pk_get(uint32_t pm, int j) { return pm >> (3 * j) & 7u; }
+template <int NS>
+RTLA_HD uint32_t perm_id_p(uint32_t v, uint32_t pim) {
+  uint32_t r = v;
+#pragma unroll
+  for (int j = 0; j < NS; j++)
+    if (v == (uint32_t)j) r = pk_get<NS>(pim, j);
+  return r;
+}
+template <int NS>
+RTLA_HD uint32_t perm_mask_p(uint32_t m, uint32_t pim) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < NS; j++) r |= ((m >> j) & 1u) << pk_get<NS>(pim, j);
+  return r;
+}
+template <int NS>
+RTLA_HD void perm_srv_rec_p(const uint32_t* rec, uint32_t pim, uint32_t invm, uint32_t* out) {
+  const uint32_t w0 = rec[0];
+  out[0] = s_make(s_term(w0), s_role(w0), perm_id_p<NS>(s_voted(w0), pim), s_commit(w0),
+                  perm_mask_p<NS>(s_vresp(w0), pim), perm_mask_p<NS>(s_vgrant(w0), pim),
+                  perm_mask_p<NS>(s_vlp(w0), pim));
+  out[1] = rec[1];
+  uint32_t nm = 0;
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    const int j = (int)pk_get<NS>(invm, k);  // field k of the image = field j of the original
+    nm |= nm_next(rec[2], j) << (3 * k) | nm_match(rec[2], j) << (15 + 3 * k);
+    out[3 + k] = sel_word<NS>(rec + 3, j);
+  }
+  out[2] = nm;
+}
+template <int NS>
+RTLA_HD uint64_t perm_msg_slot_p(const Layout& L, uint64_t v, uint32_t pim) {
+  if (!v) return 0;  // empty slot (h_msg(0) = 0)
+  const uint64_t m = (1ull << L.b_sid) - 1ull;
+  const uint32_t src = (uint32_t)(v >> 2 & m), dst = (uint32_t)(v >> (2 + L.b_sid) & m);
+  return (v & ~(m << 2 | m << (2 + L.b_sid))) | (uint64_t)perm_id_p<NS>(src, pim) << 2 |
+         (uint64_t)perm_id_p<NS>(dst, pim) << (2 + L.b_sid);
+}
+template <int NS>
+RTLA_HD void perm_elec_p(const uint32_t* e, uint32_t pim, uint32_t invm, uint32_t* out) {
+  const uint32_t w0 = e[0];
+  out[0] = (w0 & 15u) | perm_id_p<NS>((w0 >> 4) & 7u, pim) << 4 | perm_mask_p<NS>((w0 >> 7) & 31u, pim) << 7 |
+           perm_mask_p<NS>((w0 >> 12) & 31u, pim) << 12;
+  out[1] = e[1];
+#pragma unroll
+  for (int k = 0; k < NS; k++) out[2 + k] = sel_word<NS>(e + 2, (int)pk_get<NS>(invm, k));
+}
+
+// The orbit key of a state given through accessors:
+//   rec_of(i, out)  server i's record (3 + NS words)
+//   slot_of(q)      bag slot q < nmsg, PACKED (0 = empty)
+//   elec_of(e, out) election record e < nelec (2 + NS words)
+//   afp             fingerprint of allLogs (permutation-free)
+// `perms` (optional) receives |C(s)|.
 template <int NS, class RecF, class SlotF, class ElecF>
 RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
                    int* perms = nullptr) {
@@ -1432,14 +1493,18 @@ RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int ne
     }
   }
 #pragma unroll
-  for (int i = 0; i < NS; i++) {
+  for (int j = 0; j < NS; j++) sig[j] = 0;
+#pragma unroll 1
+  for (int i = 0; i < NS; i++) {  // one record live at a time
     uint32_t rec[SW];
     rec_of(i, rec);
-    sig[i] = (uint64_t)srv_sig<NS>(i, rec) << 32 | mix32(ms[i] ^ mix32(mr[i] + 0x27d4eb2fu));
+    const uint64_t si = (uint64_t)srv_sig<NS>(i, rec) << 32 | mix32(sel_word<NS>(ms, i) ^ mix32(sel_word<NS>(mr, i) + 0x27d4eb2fu));
+    set_at<NS>(sig, i, si);
   }
   // pi[i] ranges over [lo_i, lo_i + cnt_i); server i picks among the
   // positions its tie group has left: rad_i = cnt_i - (tied servers before i)
-  int lo[NS], cnt[NS], rad[NS];
+  // (lo, cnt, rad packed 3 bits per server)
+  uint32_t lom = 0, cntm = 0, radm = 0;
   int ncomb = 1;
 #pragma unroll
   for (int i = 0; i < NS; i++) {
@@ -1450,25 +1515,25 @@ RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int ne
       c += sig[j] == sig[i] ? 1 : 0;
       if (j < i) b += sig[j] == sig[i] ? 1 : 0;
     }
-    lo[i] = l;
-    cnt[i] = c;
-    rad[i] = c - b;
+    lom |= (uint32_t)l << (3 * i);
+    cntm |= (uint32_t)c << (3 * i);
+    radm |= (uint32_t)(c - b) << (3 * i);
     ncomb *= c - b;
   }
   if (perms) *perms = ncomb;
   FP best{~0ull, ~0ull};
   for (int k = 0; k < ncomb; k++) {
-    int pi[NS], inv[NS];
-    uint32_t used = 0;
+    uint32_t pim = 0, invm = 0, used = 0;
     int rem = k;
 #pragma unroll
     for (int i = 0; i < NS; i++) {
+      const int rad = (int)pk_get<NS>(radm, i), cnt = (int)pk_get<NS>(cntm, i), lo = (int)pk_get<NS>(lom, i);
       int dgt = 0;
-      if (rad[i] > 1) {
-        dgt = rem % rad[i];
-        rem /= rad[i];
+      if (rad > 1) {
+        dgt = rem % rad;
+        rem /= rad;
       }
-      const uint32_t free = ((1u << cnt[i]) - 1u) << lo[i] & ~used;
+      const uint32_t free = ((1u << cnt) - 1u) << lo & ~used;
       int p = 0, c = dgt;
 #pragma unroll
       for (int b = 0; b < NS; b++)
@@ -1476,27 +1541,23 @@ RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int ne
           if (c == 0) p = b;
           c--;
         }
-      pi[i] = p;
+      pim |= (uint32_t)p << (3 * i);
+      invm |= (uint32_t)i << (3 * p);
       used |= 1u << p;
     }
-#pragma unroll
-    for (int i = 0; i < NS; i++)
-#pragma unroll
-      for (int j = 0; j < NS; j++)
-        if (pi[j] == i) inv[i] = j;
     FP f{0, 0};
-#pragma unroll
+#pragma unroll 1
     for (int i = 0; i < NS; i++) {
       uint32_t rec[SW], out[SW];
       rec_of(i, rec);
-      perm_srv_rec<NS>(rec, pi, inv, out);
-      f = fp_add(f, hash_words_from<SW>(srv_seed<NS>(pi[i]), out));
+      perm_srv_rec_p<NS>(rec, pim, invm, out);
+      f = fp_add(f, hash_words_from<SW>(srv_seed<NS>((int)pk_get<NS>(pim, i)), out));
     }
-    for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot<NS>(L, slot_of(q), pi)));
+    for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot_p<NS>(L, slot_of(q), pim)));
     for (int e = 0; e < nelec; e++) {
       uint32_t er[EW], out[EW];
       elec_of(e, er);
-      perm_elec<NS>(er, pi, inv, out);
+      perm_elec_p<NS>(er, pim, invm, out);
       f = fp_add(f, h_elec(out, EW));
     }
     if (fp_less(f, best)) best = f;

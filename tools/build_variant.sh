@@ -10,10 +10,10 @@ F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
 S=$ROOT/raft-tla_amd/csrc
 for u in rtla_kernels rtla_kwave rtla_kpack rtla_kspec_a rtla_kspec_b rtla_ksym_a rtla_ksym_b rtla_kgeneric_a \
          rtla_kgeneric_b; do
-  $H $F -c -o $D/$u.o $S/$u.hip &
+  $H $F -c -o $D/$u.o $S/$u.hip & pids="$pids $!"
 done
-$H $F -c -o $D/h.o $S/rtla_host.cpp &
-$H $F -c -o $D/t.o $S/rtla_text.cpp &
-wait
+$H $F -c -o $D/h.o $S/rtla_host.cpp & pids="$pids $!"
+$H $F -c -o $D/t.o $S/rtla_text.cpp & pids="$pids $!"
+for p in $pids; do wait $p || { echo "build_variant: a unit failed"; exit 1; }; done
 $H -shared -fPIC --offload-arch=gfx950 -o $D/librtla.so $D/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f $D/*.o
