@@ -35,8 +35,11 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
       const unsigned long long i = p * cap + k;
       const FP f{recv_fp[2 * i], recv_fp[2 * i + 1]};
       if (f.a | f.b) {  // 0:0 = a hole in the sender's outbox chunk
-        r = fpset_insert(table, tlog2, f);
-        if (r < 0) set_flag(ctr, FLAG_FPSET_FULL);
+        // load first (the owner may know the state already: a plain load is
+        // cheaper than an atomic at the memory side), CAS only an empty slot
+        const unsigned long long key = f.b | 1ull, idx = f.a >> (64 - tlog2);
+        const unsigned long long seen = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r = fpset_resolve_loaded(table, tlog2, key, idx, seen, ctr) ? 1 : 0;
         probes++;
       }
     }

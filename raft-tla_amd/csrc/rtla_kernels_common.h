@@ -232,33 +232,40 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
   return (unsigned long long)lo | (unsigned long long)hi << 32;
 }
 
-// SYMMETRY: orbit key of the successor parent + d (allLogs' fingerprint
-// afp), without materialising it (rtla_model.h sym_key).
-template <int NS, class P>
-__device__ __forceinline__ FP successor_orbit_key(const Layout& L, P prow, const DeltaT<NS>& d, FP afp) {
+// SYMMETRY: the successor parent + d through sym_key's accessors (server
+// records, bag slots, election records), without materialising it:
+// f(rec_of, nmsg, slot_of, nelec, elec_of).
+template <int NS, class P, class F>
+__device__ __forceinline__ auto with_successor(const Layout& L, P prow, const DeltaT<NS>& d, F f) {
   constexpr int EW = 2 + NS;
   const int ne0 = row_nelec(L, prow);
-  return sym_key<NS>(
-      L, [&](int i, uint32_t* out) {
-        load_rec<NS>(L, prow, i, out);
-        if (i == d.srv) {
+  auto rec_of = [&](int i, uint32_t* out) {
+    load_rec<NS>(L, prow, i, out);
+    if (i == d.srv) {
 #pragma unroll
-          for (int w = 0; w < 3 + NS; w++) out[w] = d.rec[w];
-        }
-      },
-      d.nmsg, [&](int q) { return bag_get(L, prow, d, q); }, ne0 + (d.elec ? 1 : 0),
-      [&](int e, uint32_t* out) {
-        if (e < ne0) {
-          out[0] = elec_w0(L, prow, e);
-          out[1] = elec_log(L, prow, e);
+      for (int w = 0; w < 3 + NS; w++) out[w] = d.rec[w];
+    }
+  };
+  auto slot_of = [&](int q) { return bag_get(L, prow, d, q); };
+  auto elec_of = [&](int e, uint32_t* out) {
+    if (e < ne0) {
+      out[0] = elec_w0(L, prow, e);
+      out[1] = elec_log(L, prow, e);
 #pragma unroll
-          for (int j = 0; j < NS; j++) out[2 + j] = elec_vl(L, prow, e, j);
-        } else {
+      for (int j = 0; j < NS; j++) out[2 + j] = elec_vl(L, prow, e, j);
+    } else {
 #pragma unroll
-          for (int w = 0; w < EW; w++) out[w] = d.erec[w];
-        }
-      },
-      afp);
+      for (int w = 0; w < EW; w++) out[w] = d.erec[w];
+    }
+  };
+  return f(rec_of, d.nmsg, slot_of, ne0 + (d.elec ? 1 : 0), elec_of);
+}
+// Orbit key of the successor parent + d (allLogs' fingerprint afp).
+template <int NS, class P>
+__device__ __forceinline__ FP successor_orbit_key(const Layout& L, P prow, const DeltaT<NS>& d, FP afp) {
+  return with_successor<NS>(L, prow, d, [&](auto rec_of, int nmsg, auto slot_of, int nelec, auto elec_of) {
+    return sym_key<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of, afp);
+  });
 }
 
 // Load the parent row into LDS and derive the per-parent data every lane
@@ -416,7 +423,7 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #define RTLA_COMPACT_WAVES_PER_EU 3  // 166 VGPRs for N = 3 without spills (the default allocation took 170 -> 2 waves)
 #endif
 #ifndef RTLA_SYM_WAVES_PER_EU
-#define RTLA_SYM_WAVES_PER_EU 2      // SYMMETRY: the full Delta and the orbit-key loop stay in VGPRs
+#define RTLA_SYM_WAVES_PER_EU 3      // SYMMETRY: 168 VGPRs with spills beats 256 without (configs[3]: 356 vs 406 ms)
 #endif
 #ifndef RTLA_MULTI_ASYNC
 #define RTLA_MULTI_ASYNC 1  // multi-shard kernels pipeline their CAS too
@@ -541,7 +548,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // next-level slot reservation for all of them (slots past next_cap are
   // dropped and flagged: the level is then reported incomplete):
   //  (1) the wave copies each parent row (LDS) to its child's slot with
-  //      coalesced stores, for all of them;
+  //      coalesced stores, for all of them (copying per batch of 64 instead,
+  //      so that the patches reach lines still in L2, was measured: no
+  //      fewer HBM writes, 5 % slower);
   //  (2) per batch of 64, one state per lane: its full Delta (compute_delta
   //      with slot bookkeeping; the probe pass only folded it into a hash),
   //      fingerprint, invariants and distinct coverage -- the first batch's
@@ -562,11 +571,12 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     const unsigned long long p0 = ring_idx(next, obase);
     const int n1 = (int)min<unsigned long long>(next.cap - p0, (unsigned long long)nrows) * W;  // words before the wrap
     uint32_t* d1 = next.base + p0 * (unsigned long long)W;
-    if (rows_on) {  // (1): word i of the run of nrows child rows, lane-contiguous
-      const int nwords = nrows * W;
-      int r = 0, w = lane;
+    // (1) for child rows [rb, re): word i of the run, lane-contiguous
+    auto copy_rows = [&](int rb, int re) {
+      const int nwords = re * W;
+      int r = rb, w = lane;
       while (w >= W) { w -= W; r++; }
-      for (int i0 = 0; i0 < nwords; i0 += 64) {
+      for (int i0 = rb * W; i0 < nwords; i0 += 64) {
         const int i = i0 + lane;
         if (i < nwords) {
           const int sr = newl[(head + r) & (NEWCAP - 1)] >> 8;
@@ -577,7 +587,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         w += 64;
         while (w >= W) { w -= W; r++; }
       }
-    }
+    };
+    if (rows_on) copy_rows(0, nrows);  // (all of them first: one pass of coalesced stores)
     for (int b = 0; b < ntot; b += 64) {  // (2), (3)
       const bool act = b + lane < ntot;
       const int e = act ? newl[(head + b + lane) & (NEWCAP - 1)] : 0;
@@ -837,8 +848,12 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // SYMMETRY: the orbit keys of kring[kd, kd + kc), one per lane: the full
   // Delta (the probe pass only folded it into a hash), then
   // successor_orbit_key; the key goes through the probe pipeline.  Kept
-  // apart from the evaluation so that neither pass holds the other's
-  // registers.
+  // apart from the evaluation pass so that neither holds the other's
+  // registers.  (Spreading a chunk's permutation images over the wave --
+  // reachable configs[3] states compare 2.2 images on average but the
+  // slowest of 64 lanes 7.5 -- was built and measured: 2.1-2.4x slower, the
+  // recomputed Deltas and the LDS min-reduction cost more than the
+  // divergence they remove.)
   auto key_chunk = [&](int kd, int kc) {
     const bool active = lane < kc;
     const int e = active ? kring[(kd + lane) & (RING - 1)] : 0;
@@ -962,6 +977,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           if (KSPLIT && kpos - kdone >= 64) {  // 64 orbit keys are queued: key them (they feed the probe pipeline)
             key_chunk(kdone, 64);
             kdone += 64;
+            STAMP(7);  // SYMMETRY: orbit keys
           }
           resolve();  // the previous chunk's probes, after this chunk's arithmetic
           STAMP(3);
@@ -988,6 +1004,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     uint32_t pfa = 0, pfb = 0;
     if (KSPLIT && kpos > kdone) {  // the group's last orbit keys
       key_chunk(kdone, kpos - kdone);
+      STAMP(7);
       resolve();
       issue_probe();
       kdone = kpos;
@@ -1024,7 +1041,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   for (int off = 32; off > 0; off >>= 1) my_cas += __shfl_down(my_cas, off);
   if (lane == 0 && my_cas) atomicAdd(&ctr->cas, (unsigned long long)my_cas);
 #endif
-  STAMP(7);
+  STAMP(7);  // (kernel end: negligible)
   RTLA_STAMP_FLUSH(ctr, lane)
   __syncthreads();
   for (int k = threadIdx.x; k < 2 * COVER_CODES; k += blockDim.x)

@@ -1402,12 +1402,6 @@ RTLA_HD FP orbit_key_finish(FP m) {
   return FP{mix_a(m.a ^ (m.b >> 29 | m.b << 35)), mix_b(m.b)};
 }
 
-// The orbit key of a state given through accessors:
-//   rec_of(i, out)  server i's record (3 + NS words)
-//   slot_of(q)      bag slot q < nmsg, PACKED (0 = empty)
-//   elec_of(e, out) election record e < nelec (2 + NS words)
-//   afp             fingerprint of allLogs (permutation-free)
-// `perms` (optional) receives |C(s)|.
 // Permutations packed 3 bits per server (pim: pi[j] at bits 3j, invm: its
 // inverse), so a loop over servers indexes them with shifts: the orbit-key
 // loops below stay rolled (one record live at a time) instead of unrolling
@@ -1468,11 +1462,17 @@ RTLA_HD void perm_elec_p(const uint32_t* e, uint32_t pim, uint32_t invm, uint32_
 //   slot_of(q)      bag slot q < nmsg, PACKED (0 = empty)
 //   elec_of(e, out) election record e < nelec (2 + NS words)
 //   afp             fingerprint of allLogs (permutation-free)
-// `perms` (optional) receives |C(s)|.
-template <int NS, class RecF, class SlotF, class ElecF>
-RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
-                   int* perms = nullptr) {
-  constexpr int SW = 3 + NS, EW = 2 + NS;
+// in two phases: sym_rank (the signatures and the tie groups they leave:
+// C(s) has `ncomb` members) and sym_image_fp (the fingerprint of pi_k(s)
+// for the k-th member), so that a kernel can spread the images of a chunk's
+// states over its lanes.  sym_key = both.
+struct SymRank {
+  uint32_t lom, cntm, radm;  // per server (3 bits each): first position, tie-group size, choices left
+  int ncomb;                 // |C(s)|
+};
+template <int NS, class RecF, class SlotF>
+RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of) {
+  constexpr int SW = 3 + NS;
   // signatures: local part (high half) | sent/received message multisets
   uint32_t ms[NS], mr[NS];
   uint64_t sig[NS];
@@ -1503,9 +1503,7 @@ RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int ne
   }
   // pi[i] ranges over [lo_i, lo_i + cnt_i); server i picks among the
   // positions its tie group has left: rad_i = cnt_i - (tied servers before i)
-  // (lo, cnt, rad packed 3 bits per server)
-  uint32_t lom = 0, cntm = 0, radm = 0;
-  int ncomb = 1;
+  SymRank r{0, 0, 0, 1};
 #pragma unroll
   for (int i = 0; i < NS; i++) {
     int l = 0, c = 0, b = 0;
@@ -1515,51 +1513,65 @@ RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int ne
       c += sig[j] == sig[i] ? 1 : 0;
       if (j < i) b += sig[j] == sig[i] ? 1 : 0;
     }
-    lom |= (uint32_t)l << (3 * i);
-    cntm |= (uint32_t)c << (3 * i);
-    radm |= (uint32_t)(c - b) << (3 * i);
-    ncomb *= c - b;
+    r.lom |= (uint32_t)l << (3 * i);
+    r.cntm |= (uint32_t)c << (3 * i);
+    r.radm |= (uint32_t)(c - b) << (3 * i);
+    r.ncomb *= c - b;
   }
-  if (perms) *perms = ncomb;
-  FP best{~0ull, ~0ull};
-  for (int k = 0; k < ncomb; k++) {
-    uint32_t pim = 0, invm = 0, used = 0;
-    int rem = k;
+  return r;
+}
+// Fingerprint of pi_k(s), the k-th member (0 <= k < r.ncomb) of C(s).
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD FP sym_image_fp(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of,
+                        const SymRank& r, int k) {
+  constexpr int SW = 3 + NS, EW = 2 + NS;
+  uint32_t pim = 0, invm = 0, used = 0;
+  int rem = k;
 #pragma unroll
-    for (int i = 0; i < NS; i++) {
-      const int rad = (int)pk_get<NS>(radm, i), cnt = (int)pk_get<NS>(cntm, i), lo = (int)pk_get<NS>(lom, i);
-      int dgt = 0;
-      if (rad > 1) {
-        dgt = rem % rad;
-        rem /= rad;
+  for (int i = 0; i < NS; i++) {
+    const int rad = (int)pk_get<NS>(r.radm, i), cnt = (int)pk_get<NS>(r.cntm, i), lo = (int)pk_get<NS>(r.lom, i);
+    int dgt = 0;
+    if (rad > 1) {
+      dgt = rem % rad;
+      rem /= rad;
+    }
+    const uint32_t free = ((1u << cnt) - 1u) << lo & ~used;
+    int p = 0, c = dgt;
+#pragma unroll
+    for (int b = 0; b < NS; b++)
+      if (free >> b & 1u) {
+        if (c == 0) p = b;
+        c--;
       }
-      const uint32_t free = ((1u << cnt) - 1u) << lo & ~used;
-      int p = 0, c = dgt;
-#pragma unroll
-      for (int b = 0; b < NS; b++)
-        if (free >> b & 1u) {
-          if (c == 0) p = b;
-          c--;
-        }
-      pim |= (uint32_t)p << (3 * i);
-      invm |= (uint32_t)i << (3 * p);
-      used |= 1u << p;
-    }
-    FP f{0, 0};
+    pim |= (uint32_t)p << (3 * i);
+    invm |= (uint32_t)i << (3 * p);
+    used |= 1u << p;
+  }
+  FP f{0, 0};
 #pragma unroll 1
-    for (int i = 0; i < NS; i++) {
-      uint32_t rec[SW], out[SW];
-      rec_of(i, rec);
-      perm_srv_rec_p<NS>(rec, pim, invm, out);
-      f = fp_add(f, hash_words_from<SW>(srv_seed<NS>((int)pk_get<NS>(pim, i)), out));
-    }
-    for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot_p<NS>(L, slot_of(q), pim)));
-    for (int e = 0; e < nelec; e++) {
-      uint32_t er[EW], out[EW];
-      elec_of(e, er);
-      perm_elec_p<NS>(er, pim, invm, out);
-      f = fp_add(f, h_elec(out, EW));
-    }
+  for (int i = 0; i < NS; i++) {
+    uint32_t rec[SW], out[SW];
+    rec_of(i, rec);
+    perm_srv_rec_p<NS>(rec, pim, invm, out);
+    f = fp_add(f, hash_words_from<SW>(srv_seed<NS>((int)pk_get<NS>(pim, i)), out));
+  }
+  for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot_p<NS>(L, slot_of(q), pim)));
+  for (int e = 0; e < nelec; e++) {
+    uint32_t er[EW], out[EW];
+    elec_of(e, er);
+    perm_elec_p<NS>(er, pim, invm, out);
+    f = fp_add(f, h_elec(out, EW));
+  }
+  return f;
+}
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
+                   int* perms = nullptr) {
+  const SymRank r = sym_rank<NS>(L, rec_of, nmsg, slot_of);
+  if (perms) *perms = r.ncomb;
+  FP best{~0ull, ~0ull};
+  for (int k = 0; k < r.ncomb; k++) {
+    const FP f = sym_image_fp<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of, r, k);
     if (fp_less(f, best)) best = f;
   }
   return fp_add(orbit_key_finish(best), afp);
