@@ -333,6 +333,25 @@ static int comm_exchange(rtla_ctx* x, const std::vector<Msg>& sends, const std::
   return shm_barrier(x);
 }
 
+// RCCL prints its version banner on stdout when a communicator is created;
+// stdout belongs to the caller (the CLI's TLC-format output, bench.py's JSON
+// line), so the banner is sent to stderr.
+struct StdoutToStderr {
+  int saved = -1;
+  StdoutToStderr() {
+    fflush(stdout);
+    saved = dup(1);
+    if (saved >= 0) dup2(2, 1);
+  }
+  ~StdoutToStderr() {
+    fflush(stdout);
+    if (saved >= 0) {
+      dup2(saved, 1);
+      close(saved);
+    }
+  }
+};
+
 static int layout_from_cfg(const rtla_cfg* c, Layout* L) {
   if (!c) return RTLA_E_ARG;
   int K = c->bag_cap ? c->bag_cap : (c->max_msgs > 0 ? c->max_msgs + 1 : 32);
@@ -665,7 +684,12 @@ extern "C" int rtla_comm_id(void* out128) {
     return RTLA_OK;
   }
   ncclUniqueId id;
-  NCCLCHK(ncclGetUniqueId(&id));
+  ncclResult_t r0;
+  {
+    StdoutToStderr quiet;
+    r0 = ncclGetUniqueId(&id);
+  }
+  NCCLCHK(r0);
   static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
   memcpy(out128, &id, 128);
   return RTLA_OK;
@@ -776,13 +800,24 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
     } else {
       ncclUniqueId id;
       memcpy(&id, comm_id, sizeof id);
-      if (ncclCommInitRank(&x->comm, world, id, rank) != ncclSuccess) { rtla_close(x); return RTLA_E_COMM; }
+      ncclResult_t r0;
+      {
+        StdoutToStderr quiet;
+        r0 = ncclCommInitRank(&x->comm, world, id, rank);
+      }
+      if (r0 != ncclSuccess) { rtla_close(x); return RTLA_E_COMM; }
     }
   } else if (x->nshard > 1) {
     const char* tr = getenv("RTLA_TRANSPORT");
     if (tr && !strcmp(tr, "rccl")) {  // virtual shards exchanging through a one-rank RCCL communicator
       ncclUniqueId id;
-      if (ncclGetUniqueId(&id) != ncclSuccess || ncclCommInitRank(&x->comm, 1, id, 0) != ncclSuccess) {
+      ncclResult_t r0;
+      {
+        StdoutToStderr quiet;
+        r0 = ncclGetUniqueId(&id);
+        if (r0 == ncclSuccess) r0 = ncclCommInitRank(&x->comm, 1, id, 0);
+      }
+      if (r0 != ncclSuccess) {
         rtla_close(x);
         return RTLA_E_COMM;
       }
