@@ -350,9 +350,19 @@ constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a 
 // GROUP rows | allLogs' words of each state | pair ring | SYMMETRY: key ring.
 // (The outbox state exists only in the MULTI kernels: one shard's tile then
 // stays small enough for 12 one-wave blocks per CU on configs[1]'s 372-byte rows.)
+// RTLA_CHILD_STAGE > 0: child rows are built in an LDS stage of that many
+// rows (patched there, stored once).  Measured on configs[1]: HBM writes
+// 13.2 -> 10.0 GB per launch (1.09x the rows + CAS), but 197 -> 220 / 232 /
+// 286 ms per step at 16 / 32 / 64 rows (the patches run once per stage, and
+// the stage costs waves) -- so 0: copy the parent rows to HBM, then patch
+// the differing words there.
+#ifndef RTLA_CHILD_STAGE
+#define RTLA_CHILD_STAGE 0
+#endif
+constexpr int CSTAGE = RTLA_CHILD_STAGE;
 __host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym, bool multi) {
   return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW +
-          RING / 2 * (sym ? 2 : 1) + 3) & ~3;
+          RING / 2 * (sym ? 2 : 1) + CSTAGE * W + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -497,6 +507,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // queued by the evaluation pass and keyed 64 at a time (key_chunk)
   uint16_t* kring = ring + RING;
   int kpos = 0, kdone = 0;
+  uint32_t* cstage = reinterpret_cast<uint32_t*>(kring + (SYM ? RING : 0));  // CSTAGE child rows
   if (MULTI) {
     if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
@@ -588,7 +599,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         while (w >= W) { w -= W; r++; }
       }
     };
-    if (rows_on) copy_rows(0, nrows);  // (all of them first: one pass of coalesced stores)
+    if (CSTAGE == 0 && rows_on) copy_rows(0, nrows);  // (all of them first: one pass of coalesced stores)
     for (int b = 0; b < ntot; b += 64) {  // (2), (3)
       const bool act = b + lane < ntot;
       const int e = act ? newl[(head + b + lane) & (NEWCAP - 1)] : 0;
@@ -624,7 +635,37 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       }
       uint32_t spk[PACKW], epk[PACKW];  // the changed records, packed
       if (act) child_pack(L, d, spk, epk);
-      if (rows_on) {  // (3): the copies must land first (same words, other lanes)
+      if (CSTAGE > 0 && rows_on) {
+        // (1) + (3) in LDS, CSTAGE children at a time: the parent rows are
+        // copied into the stage, each child's lane patches the words in
+        // which it differs, and the wave stores the finished rows once,
+        // coalesced (no second write of any HBM line)
+        const int bn = min(64, nrows - b);
+        for (int c0 = 0; c0 < bn; c0 += CSTAGE) {
+          const int cn = min(CSTAGE, bn - c0);
+          for (int t = lane; t < cn * W; t += 64) {
+            const int r = t / W;
+            const int sr = newl[(head + b + c0 + r) & (NEWCAP - 1)] >> 8;
+            cstage[t] = rows[sr * W + (t - r * W)];
+          }
+          wave_sync();
+          if (lane >= c0 && lane < c0 + cn) {
+            const StridedWords<GROUP> pall_p{pall + sl};
+            uint32_t* dst = cstage + (lane - c0) * W;
+            child_write(L, rows + sl * W, d, spk, epk, pall_p, cfp, [&](int w, uint32_t v) { dst[w] = v; });
+          }
+          wave_sync();
+          const int off0 = (b + c0) * W;
+          for (int t = lane; t < cn * W; t += 64) {
+            const int i = off0 + t;
+            const uint32_t v = cstage[t];
+            if (i < n1) d1[i] = v;
+            else next.base[i - n1] = v;
+          }
+          wave_sync();  // (the stage is refilled next)
+        }
+      }
+      if (CSTAGE == 0 && rows_on) {  // (3): the copies must land first (same words, other lanes)
         if (b == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (child < nrows) {
           const StridedWords<GROUP> pall_p{pall + sl};
