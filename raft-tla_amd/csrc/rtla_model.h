@@ -1466,12 +1466,54 @@ RTLA_HD void perm_elec_p(const uint32_t* e, uint32_t pim, uint32_t invm, uint32_
 // C(s) has `ncomb` members) and sym_image_fp (the fingerprint of pi_k(s)
 // for the k-th member), so that a kernel can spread the images of a chunk's
 // states over its lanes.  sym_key = both.
+#ifndef RTLA_TWIN_MIN
+#define RTLA_TWIN_MIN 3  // smallest tie group sym_rank tests for interchangeable members
+#endif
 struct SymRank {
   uint32_t lom, cntm, radm;  // per server (3 bits each): first position, tie-group size, choices left
   int ncomb;                 // |C(s)|
 };
-template <int NS, class RecF, class SlotF>
-RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of) {
+// Is the transposition (i j) an automorphism of s -- tau(s) = s -- by a
+// SUFFICIENT test: no message names i or j, every election record and every
+// other server's record is unchanged by the relabelling, and i's record
+// relabelled is j's.  (Then all orderings of a tie group whose consecutive
+// members pass give the same image: the transpositions generate the group's
+// permutations.  A test that fails merely keeps all of them.)
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD bool sym_twins(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, int i,
+                       int j) {
+  constexpr int SW = 3 + NS, EW = 2 + NS;
+  const uint64_t sm = (1ull << L.b_sid) - 1ull;
+  for (int q = 0; q < nmsg; q++) {
+    const uint64_t v = slot_of(q);
+    if (!v) continue;
+    const uint32_t src = (uint32_t)(v >> 2 & sm), dst = (uint32_t)(v >> (2 + L.b_sid) & sm);
+    if (src == (uint32_t)i || src == (uint32_t)j || dst == (uint32_t)i || dst == (uint32_t)j) return false;
+  }
+  uint32_t tau = 0;  // the transposition, packed (its own inverse)
+#pragma unroll
+  for (int k = 0; k < NS; k++) tau |= (uint32_t)(k == i ? j : k == j ? i : k) << (3 * k);
+  bool same = true;
+#pragma unroll 1
+  for (int p = 0; p < NS; p++) {  // relabel(rec_p) == rec_{tau(p)}
+    uint32_t a[SW], b[SW], out[SW];
+    rec_of(p, a);
+    rec_of(p == i ? j : p == j ? i : p, b);
+    perm_srv_rec_p<NS>(a, tau, tau, out);
+#pragma unroll
+    for (int w = 0; w < SW; w++) same = same && out[w] == b[w];
+  }
+  for (int e = 0; e < nelec && same; e++) {
+    uint32_t er[EW], out[EW];
+    elec_of(e, er);
+    perm_elec_p<NS>(er, tau, tau, out);
+#pragma unroll
+    for (int w = 0; w < EW; w++) same = same && out[w] == er[w];
+  }
+  return same;
+}
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of) {
   constexpr int SW = 3 + NS;
   // signatures: local part (high half) | sent/received message multisets
   uint32_t ms[NS], mr[NS];
@@ -1517,6 +1559,30 @@ RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of) 
     r.cntm |= (uint32_t)c << (3 * i);
     r.radm |= (uint32_t)(c - b) << (3 * i);
     r.ncomb *= c - b;
+  }
+  if (r.ncomb > 1) {
+    // tie groups whose members are interchangeable (sym_twins for each
+    // member and the next one of its group) need one ordering only
+#pragma unroll 1
+    for (int i = 0; i < NS; i++) {
+      const uint32_t li = pk_get<NS>(r.lom, i), ci = pk_get<NS>(r.cntm, i);
+      // i: first member of a tie group of >= RTLA_TWIN_MIN (a pair's test
+      // costs about what its second image does)
+      if (ci < RTLA_TWIN_MIN || pk_get<NS>(r.radm, i) != ci) continue;
+      bool all = true;
+      int prev = i;
+      for (int j = i + 1; j < NS && all; j++) {
+        if (pk_get<NS>(r.lom, j) != li) continue;  // (same first position <=> same group)
+        all = sym_twins<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of, prev, j);
+        prev = j;
+      }
+      if (!all) continue;
+      for (int j = i; j < NS; j++)
+        if (pk_get<NS>(r.lom, j) == li) r.radm = (r.radm & ~(7u << (3 * j))) | 1u << (3 * j);
+    }
+    r.ncomb = 1;
+#pragma unroll
+    for (int i = 0; i < NS; i++) r.ncomb *= (int)pk_get<NS>(r.radm, i);
   }
   return r;
 }
@@ -1567,7 +1633,7 @@ RTLA_HD FP sym_image_fp(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, i
 template <int NS, class RecF, class SlotF, class ElecF>
 RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
                    int* perms = nullptr) {
-  const SymRank r = sym_rank<NS>(L, rec_of, nmsg, slot_of);
+  const SymRank r = sym_rank<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of);
   if (perms) *perms = r.ncomb;
   FP best{~0ull, ~0ull};
   for (int k = 0; k < r.ncomb; k++) {
