@@ -115,15 +115,16 @@ def load_traffic(workload):
     return best
 
 
-def fpset_log2_for(workload, world, override=0, shards=0):
+def fpset_log2_for(workload, world, override=0, shards=0, pinned=True):
     """log2 fingerprint-set slots per rank (per shard): the workload's
     single-GPU size, divided by the next power of two >= world (each rank owns
     1/world of the fingerprints, so the load stays ~28 %); an explicit override
-    is per rank.  Capped workloads keep the single-GPU size per rank: with
-    more GPUs they reach deeper levels.  Virtual shards on one GPU (--shards S)
-    split the single-GPU set S ways, as S ranks would."""
+    is per rank.  A capped workload run to the depth that fits (--depth fit,
+    not `pinned`) keeps the single-GPU size per rank: with more GPUs it
+    reaches deeper levels.  Virtual shards on one GPU (--shards S) split the
+    single-GPU set S ways, as S ranks would."""
     fpl = override or FPSET_LOG2.get(workload, 30)
-    if not override and world > 1 and workload not in CAPPED:
+    if not override and world > 1 and (workload not in CAPPED or pinned):
         fpl = max(24, fpl - (world - 1).bit_length())
     if not override and shards > 1:
         fpl = max(24, fpl - (shards - 1).bit_length())
@@ -228,7 +229,8 @@ class Run:
         self.shape = WORKLOADS[name]
         self.capped = name in CAPPED
         n, v, t, l, c, m, inv = self.shape
-        self.fpl = fpset_log2_for(name, world, args.fpset_log2, args.shards)
+        self.fpl = fpset_log2_for(name, world, args.fpset_log2, args.shards,
+                                  pinned=args.depth == "pinned" and name in PINNED_LEVELS)
         self.cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=self.fpl, shards=args.shards,
                                bag_cap=BAG_CAP.get(name, 0), frontier_cap=frontier_cap,
                                symmetry=name in SYMMETRIC,
