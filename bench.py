@@ -234,7 +234,8 @@ class Run:
         self.cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=self.fpl, shards=args.shards,
                                bag_cap=BAG_CAP.get(name, 0), frontier_cap=frontier_cap,
                                symmetry=name in SYMMETRIC,
-                               mem_budget=(200 << 30) if args.shards > 1 else 0)
+                               mem_budget=(args.mem_budget << 30) if args.mem_budget else
+                               (200 << 30) if args.shards > 1 else 0)
         self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
         self.levels_cap = None   # complete levels a capped search reaches
         self.pinned = PINNED_LEVELS.get(name) if args.depth == "pinned" else None
@@ -405,6 +406,9 @@ def main():
     ap.add_argument("--fpset-log2", type=int, default=0,
                     help="log2 fingerprint-set slots per rank (TLC's -fpmem analogue); 0 = sized to the workload")
     ap.add_argument("--frontier-cap", type=int, default=0, help="rows of the frontier arena per rank (0 = auto)")
+    ap.add_argument("--mem-budget", type=int, default=0,
+                    help="device memory per rank in GiB (0 = 85 %% of what is free; several ranks sharing one GPU, "
+                         "e.g. over RTLA_TRANSPORT=shm, need a share each)")
     ap.add_argument("--levels", action="store_true", help="print the per-level tables to stderr")
     ap.add_argument("--synth-states", type=int, default=SYNTH_STATES,
                     help="synthetic workload: input states per GPU")
