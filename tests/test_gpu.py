@@ -753,3 +753,25 @@ def test_synthetic_resident_dedup_matches_step():
     with pytest.raises(rtla.RtlaError):
         with rtla.Checker(cfg) as ck:
             ck.synthetic_dedup(10, n)  # not a group boundary
+
+
+def test_bench_gpus2_over_shm_matches_golden():
+    """The driver's multi-GPU entry point itself: `bench.py --gpus 2` (two
+    ranks under torch.distributed.run, gloo control plane, the checker's own
+    exchange -- here over the shared-memory transport, both ranks on this
+    GPU) exhausts a model with the golden counts and prints one JSON line."""
+    import subprocess
+    import sys
+    g = GOLD["n3_v1_t2_l1_m1"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RTLA_TRANSPORT="shm", RTLA_SHM_SLOT_MB="32")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload",
+                        "raft3_v1_t2_l1_m1", "--mem-budget", "8", "--no-cpu", "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    c = r["config"]
+    assert r["n_gpus"] == 2 and c["parallelism"] == "fp-sharded2" and c["exhausted"]
+    assert (c["distinct"], c["generated"], c["depth"]) == (g["distinct"], g["generated"], g["depth"])
