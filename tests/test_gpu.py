@@ -766,7 +766,8 @@ def test_bench_gpus2_over_shm_matches_golden():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, RTLA_TRANSPORT="shm", RTLA_SHM_SLOT_MB="32")
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload",
-                        "raft3_v1_t2_l1_m1", "--mem-budget", "8", "--no-cpu", "--steps", "1", "--warmup", "0"],
+                        "raft3_v1_t2_l1_m1", "--mem-budget", "8", "--fpset-log2", "24", "--no-cpu", "--steps", "1",
+                        "--warmup", "0"],
                        env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
