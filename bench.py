@@ -87,12 +87,13 @@ SYNTH_STATES = 125_000_000
 SYNTH_POOL_FRAC = 10
 SYNTH_BATCH = 1 << 24
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-# Random 8-byte fingerprint-set accesses into a 32 GiB table (far beyond the
-# 256 MiB Infinity Cache), all CUs, measured on MI355X by tools/probe_calib.py
-# (profiles/r01_v5/calib.log): CAS ~1.55e10/s (insert or
-# present), load of a present key ~4.66e10/s.  The probe kernel loads the home
-# slot and CASes only empty slots, so its ceiling for P probes of which D
-# find new states is P / (P / LOAD + D / CAS).
+# Pure-stream rates of random 8-byte fingerprint-set accesses into a 32 GiB
+# table, all CUs, measured on MI355X by tools/probe_calib.py
+# (profiles/r01_v5/calib.log): CAS ~1.55e10/s, load of a present key
+# ~4.66e10/s.  Only the fallback model P / (P / LOAD + D / CAS) when the live
+# calibration is skipped (--no-calib): the random-access ceiling is MEASURED
+# in the same run (calibrate_probes), on a mixed stream at the workload's own
+# insert fraction.
 CAS_PER_S = 1.55e10
 LOAD_PER_S = 4.66e10
 
@@ -220,6 +221,29 @@ def cpu_baseline(shape, sample_states, threads):
                       % (len(r["levels"]), r["distinct"], r["generated"], r["seconds"], threads)}
 
 
+def cpu_baseline_synthetic(rtla, cfg, pool, threads, target_s=12.0):
+    """The synthetic microbench's CPU leg: the same random input states
+    (rtla_random_texts: the generator's rows printed as state text, outside
+    the timed region) parsed by the C oracle and run through Next + dedup
+    into one seen set (oracle/raft_cpu.c orc_dedup_texts) -- batches until
+    ~target_s seconds of oracle time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import raft_cpu
+    n, v, t, l, c, m, inv = WORKLOADS["synthetic"]
+    d = raft_cpu.Dedup(raft_cpu.cfg_of(n, v, t, l, c, m, inv))
+    first, batch = 0, 1 << 16
+    while d.seconds < target_s and first < (16 << 20):
+        d.batch(rtla.random_texts(cfg, first, batch, pool), batch, threads)
+        first += batch
+    gen, probes, new = d.counts
+    d.close()
+    return {"value": first / d.seconds, "unit": "input states/s", "cores": threads,
+            "host_cpus": os.cpu_count(), "cgroup_cpu_quota": cpu_quota(), "kind": "port",
+            "sample": "input states 0..%d of the same generator (pool %d), oracle/raft_cpu.c Next + dedup on %d "
+                      "threads: %d generated, %d probes, %d new in %.1f s" % (first - 1, pool, threads, gen, probes,
+                                                                             new, d.seconds)}
+
+
 class Run:
     """A checker context for one workload, and how to time it."""
 
@@ -303,7 +327,33 @@ def timed(run, steps, warmup, world, barrier, cap_levels=0):
     return max_over_ranks(t1 - t0, world) / steps, levels
 
 
-def roofline(levels, world, workload):
+def calibrate_probes(fpl, n_present, probes, new):
+    """The random-access ceiling, measured live (rtla_probe_bench3): a table
+    of the workload's size (2^fpl slots) holding n_present keys -- what the
+    fingerprint set holds when the run's largest level kernel starts -- then
+    a timed stream of uniformly random load-first probes (load the home slot,
+    CAS only an empty one), a fraction new / probes of them new keys: the
+    level kernel's own mix.  Probes/s of that stream = the ceiling."""
+    import rtla
+    n = int(min(max(probes, 1 << 24), 1 << 30))
+    q = new / probes if probes else 0.0
+    n_present = int(min(n_present, (1 << fpl) // 2))
+    sec, ins = rtla.probe_mixed(fpl, n_present, n, q)
+    return {"ceiling_per_s": n / sec, "new_frac": q, "table_slots_log2": fpl, "present_keys": n_present,
+            "probes": n, "inserted": ins, "seconds": sec,
+            "source": "live: rtla_probe_bench3 (uniform random load-first probes, CAS on an empty slot, "
+                      "this run, this GPU)"}
+
+
+def calib_inputs(levels):
+    """(keys in the set when the largest level kernel starts, probes, new) of a run."""
+    lv1 = levels[1:]
+    big = max(range(len(lv1)), key=lambda k: lv1[k].probes) if lv1 else 0
+    present = sum(lv.new for lv in levels[:big + 1])
+    return present, sum(lv.probes for lv in lv1), sum(lv.new for lv in lv1)
+
+
+def roofline(levels, world, workload, calib=None):
     """Roofline of the dominant kernel -- k_expand_compact, the whole BFS
     level (expand, fingerprint, probe, insert, build the new rows) -- from
     the last run's HIP-event times around it (expand_ms).  Algorithmic bytes
@@ -320,7 +370,12 @@ def roofline(levels, world, workload):
     kernel_bytes = E * S + P * 64 + D * (S + 8)
     achieved = kernel_bytes / world / (ems / 1e3) / 1e9   # per GPU
     traffic = load_traffic(workload) if world == 1 else None
-    ra_ceiling = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
+    if calib:
+        ra_ceiling, ra_model, ra_source = calib["ceiling_per_s"], "measured mixed stream (calibration)", calib["source"]
+    else:
+        ra_ceiling = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
+        ra_model = "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S) (--no-calib fallback)"
+        ra_source = "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)"
     return {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
@@ -333,8 +388,7 @@ def roofline(levels, world, workload):
         "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + D*(S+8) new rows and parent records",
         "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
                           "frac": P / world / (ems / 1e3) / ra_ceiling,
-                          "model": "load-first probes: P / (P / LOAD_PER_S + D / CAS_PER_S)",
-                          "source": "tools/probe_calib.py on MI355X (profiles/r01_v5/calib.log)",
+                          "model": ra_model, "source": ra_source, "calibration": calib,
                           # SURVEY.md 8(d)'s probe term: probes / (t * the calibrated random 8-B CAS rate)
                           "frac_vs_cas_rate": P / world / (ems / 1e3) / CAS_PER_S},
     }
@@ -420,6 +474,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous check only: every rank joins the process group, receives rank 0's "
                          "RCCL-id payload, prints one line and exits (no GPU work; used by the CPU tests)")
+    ap.add_argument("--no-calib", action="store_true",
+                    help="skip the live random-access calibration (the ceiling then comes from the pure-stream model)")
     ap.add_argument("--shards", type=int, default=0,
                     help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
                          "(the multi-GPU exchange protocol with device copies as transport)")
@@ -466,7 +522,10 @@ def main():
         ems = tot["kernel_ms"]
         P, D = tot["probes"], tot["new"]
         kbytes = n * S + P * 64
-        ra = P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S
+        straffic = load_traffic("synthetic")
+        run.ck.close()
+        calib = None if args.no_calib else calibrate_probes(run.fpl, D // 2, P, D)
+        ra = calib["ceiling_per_s"] if calib else (P / (P / LOAD_PER_S + D / CAS_PER_S) if P else LOAD_PER_S)
         out = {
             "metric": "random packed states/sec through Next + fingerprint + dedup (BASELINE configs[4])",
             "value": n * world / per_step, "unit": "input states/s", "n_gpus": world, "steps": args.steps,
@@ -481,18 +540,24 @@ def main():
                        "fpset_slots_log2": run.fpl,
                        "parallelism": "single" if world == 1 else "replicas%d" % world},
             "roofline": {"bound": "hbm", "achieved": kbytes / (ems / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": kbytes / (ems / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "frac": kbytes / (ems / 1e3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": straffic["bytes_per_launch"] if straffic else None,
+                         "traffic_source": straffic["source"] if straffic else None,
                          "kernel": "k_expand_compact (XF_DEDUP_ONLY)", "launches": tot["batches"],
                          "kernel_ms_total": ems, "kernel_ms_avg": ems / max(1, tot["batches"]),
                          "bytes_per_launch": kbytes / max(1, tot["batches"]),
                          "model": "per launch: E*S input rows read + 64 B per fingerprint-set probe",
                          "random_access": {"probes_per_s": P / (ems / 1e3), "ceiling_per_s": ra,
-                                           "frac": P / (ems / 1e3) / ra}},
+                                           "frac": P / (ems / 1e3) / ra, "calibration": calib}},
             "cpu_baseline": None,
         }
+        if rank == 0 and world == 1 and not args.no_cpu:
+            try:
+                out["cpu_baseline"] = cpu_baseline_synthetic(rtla, run.cfg, pool, args.cpu_threads or cpu_threads())
+            except Exception as e:  # reported, never fatal for the GPU number
+                out["cpu_baseline"] = {"error": str(e)}
         if rank == 0:
             print(json.dumps(out), flush=True)
-        run.ck.close()
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
@@ -528,16 +593,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": per_step * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if run.capped else "strong",
+        # the same levels at every GPU count (oracle-pinned / --cap-levels, or a
+        # complete model check): strong scaling; --depth fit reaches deeper
+        # levels with more GPUs' memory: weak
+        "scaling": "weak" if run.capped and not run.pinned and not args.cap_levels else "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "BFS from the Init row (no input data)" + (
             ", capped at the deepest level that fits device memory" if run.capped else ", exhaustive"),
         "config": config,
-        "roofline": roofline(levels, world, args.workload),
         "cpu_baseline": None,
     }
     run.ck.close()
+    calib = None if args.no_calib else calibrate_probes(run.fpl, *calib_inputs(levels))
+    out["roofline"] = roofline(levels, world, args.workload, calib)
 
     if args.workload == DEFAULT and not args.no_secondary:
         sec = Run(rtla, SECONDARY, rank, world, comm_id, args)
@@ -549,9 +618,10 @@ def main():
                           "wall_s_to_exhaust": sec_step, "distinct": d2,
                           "generated": sum(lv.generated for lv in sec_levels),
                           "depth": sum(1 for lv in sec_levels if lv.new > 0),
-                          "distinct_per_s": d2 / sec_step,
-                          "probe_kernel": roofline(sec_levels, world, SECONDARY)}
+                          "distinct_per_s": d2 / sec_step}
         sec.ck.close()
+        scal = None if args.no_calib else calibrate_probes(sec.fpl, *calib_inputs(sec_levels))
+        out["exhaust"]["probe_kernel"] = roofline(sec_levels, world, SECONDARY, scal)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

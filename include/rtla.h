@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 7
+#define RTLA_ABI_VERSION 8
 
 /* status codes */
 #define RTLA_OK 0
@@ -166,6 +166,16 @@ int rtla_state_text(const rtla_cfg *cfg, const uint32_t *row, char *buf, size_t 
  * ranks). */
 int rtla_rows_text_hash(const rtla_cfg *cfg, const uint32_t *rows, size_t n, int threads, uint64_t *out);
 int rtla_level_text_hash(rtla_ctx *ctx, int threads, uint64_t *out);
+/* SYMMETRY level digests: the same sums over each state's ORBIT TEXT -- the
+ * text of the server-permuted image whose rotated text (the ten per-server
+ * "/\ var" lines first, then messages, elections, allLogs) is least over all
+ * N! images: a function of the orbit alone, so the orbit-count BFS's levels
+ * are compared by content with the CPU oracle's (raft_cpu.c orbit_text),
+ * whichever member of an orbit either side keeps.  Computed from the text
+ * alone, never from the kernels' orbit key.  rtla_orbit_text: one row's. */
+int rtla_rows_orbit_hash(const rtla_cfg *cfg, const uint32_t *rows, size_t n, int threads, uint64_t *out);
+int rtla_level_orbit_hash(rtla_ctx *ctx, int threads, uint64_t *out);
+int rtla_orbit_text(const rtla_cfg *cfg, const uint32_t *row, char *buf, size_t cap);
 int rtla_action_name(const rtla_cfg *cfg, int32_t inst, int32_t sub, char *buf, size_t cap);
 int rtla_invariants(const rtla_cfg *cfg, const uint32_t *row);  /* violated mask */
 /* Fingerprint of a row recomputed from scratch (the kernels derive it
@@ -204,6 +214,10 @@ int rtla_time_expand(rtla_ctx *ctx, int xflags, int reps, double *ms);
  * its inputs once and times only the dedup passes over HBM-resident rows
  * (rtla_reset clears the set, not the arena). */
 int rtla_random_rows(const rtla_cfg *cfg, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, uint32_t *rows);
+/* The same input states as state texts ('\x1e'-terminated, *len bytes in
+ * all; RTLA_E_ARG when cap is too small): the CPU baseline's input. */
+int rtla_random_texts(const rtla_cfg *cfg, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, char *buf,
+                      size_t cap, size_t *len);
 int rtla_synthetic_step(rtla_ctx *ctx, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
                         rtla_level_stats *out);
 int rtla_synthetic_generate(rtla_ctx *ctx, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool, uint64_t at);
@@ -215,6 +229,14 @@ int rtla_probe_bench(int log2, uint64_t n, double *seconds, uint64_t *inserted);
 /* n random keys inserted (CAS, all new), then re-probed (all present) with a
  * CAS and with the kernel's load-first protocol; device seconds of each pass. */
 int rtla_probe_bench2(int log2, uint64_t n, double *s_insert, double *s_seen_cas, double *s_seen_load,
+                      uint64_t *inserted);
+/* Mixed-stream calibration of the random-access ceiling: a 2^log2-slot table
+ * holding n_present random keys, then n timed probes of which a fraction
+ * new_frac are keys not in the table (inserted: load, CAS on an empty slot)
+ * and the rest keys it holds (one load) -- the level kernel's load-first
+ * protocol at a workload's own insert fraction D/P.  *seconds = the probe
+ * pass (HIP events); *inserted = keys it inserted. */
+int rtla_probe_bench3(int log2, uint64_t n_present, uint64_t n, double new_frac, double *seconds,
                       uint64_t *inserted);
 
 #ifdef __cplusplus

@@ -10,7 +10,7 @@
  *
  * Every action below cites the raft.tla line it restates
  * (/root/reference/raft.tla, sha256 683a120a...6b81).  The state constraint and
- * invariants are the build's own definitions (oracle/MC.tla), because the
+ * invariants are the build's own definitions (specs/MC.tla), because the
  * reference's raft.cfg:3 names an undefined NoTwoLeaders and has no CONSTRAINT.
  *
  * Parity status: TLC cannot run here (no JVM) and the reference ships no
@@ -592,30 +592,373 @@ static void permute_state(const orc_cfg *c, const State *s, const int *pi, State
     }
     qsort(o->elec, (size_t)s->nelec, sizeof(Elec), (int (*)(const void *, const void *))elec_cmp);
 }
-/* serialise the orbit representative of s into out; returns its length */
+/* next permutation of pi[0..N) in lexicographic order; 0 after the last */
+static int next_perm(int *pi, int N) {
+    int i = N - 2;
+    while (i >= 0 && pi[i] > pi[i + 1]) i--;
+    if (i < 0) return 0;
+    int j = N - 1;
+    while (pi[j] < pi[i]) j--;
+    int t = pi[i]; pi[i] = pi[j]; pi[j] = t;
+    for (int a = i + 1, b2 = N - 1; a < b2; a++, b2--) { t = pi[a]; pi[a] = pi[b2]; pi[b2] = t; }
+    return 1;
+}
+
+/* Orbit serialisation of the image pi(s): an injective byte encoding of the
+ * permuted state with the server fields FIRST, field-major (the N terms in
+ * position order -- position p holds server sigma[p] = pi^-1(p) -- then the
+ * N roles, then every relabelled field: votedFor, commitIndex, the vote
+ * sets, voterLog domain, log, nextIndex / matchIndex, voterLog), then the
+ * relabelled bag and elections re-sorted, then allLogs.  With `best` set,
+ * the bytes are compared with best's as they are produced: the image is
+ * dropped (returns 1) at its first byte above best's, returns 0 if it equals
+ * best, -1 if it is smaller (then the whole image is in out). */
+static int ser_image(const orc_cfg *c, const State *s, const int *pi, const int *sigma, uint8_t *out,
+                     const uint8_t *best) {
+    const int N = c->n_server;
+    int st = best ? 0 : -1;     /* 0: equal to best so far; -1: below best (or no best): write on */
+    size_t n = 0;
+#define PUT(b_)                                                             \
+    do {                                                                    \
+        const uint8_t v_ = (uint8_t)(b_);                                   \
+        if (st == 0) { if (v_ > best[n]) return 1; if (v_ < best[n]) st = -1; } \
+        out[n++] = v_;                                                      \
+    } while (0)
+#define PUTLOG(l_)                                                          \
+    do {                                                                    \
+        const Log L_ = (l_); const int k_ = log_len(L_);                    \
+        PUT(k_);                                                            \
+        for (int e_ = 1; e_ <= k_; e_++) PUT((log_term(L_, e_) << 4) | log_val(L_, e_)); \
+    } while (0)
+    for (int p = 0; p < N; p++) PUT(s->s[sigma[p]].term);
+    for (int p = 0; p < N; p++) PUT(s->s[sigma[p]].role);
+    for (int p = 0; p < N; p++) {
+        const Srv *v = &s->s[sigma[p]];
+        PUT(v->voted == NIL ? NIL : pi[v->voted]); PUT(v->commit);
+        PUT(perm_mask(v->vresp, pi, N)); PUT(perm_mask(v->vgrant, pi, N));
+        const uint8_t vlp = perm_mask(v->vlp, pi, N);
+        PUT(vlp);
+        PUTLOG(v->log);
+        for (int q = 0; q < N; q++) { PUT(v->next[sigma[q]]); PUT(v->match[sigma[q]]); }
+        for (int q = 0; q < N; q++) if (vlp >> q & 1) PUTLOG(v->vl[sigma[q]]);
+    }
+    /* bag: relabel, re-sort */
+    struct { Msg m; uint8_t cnt; } bag[KMAX];
+    for (int k = 0; k < s->nmsg; k++) {
+        bag[k].m = s->msg[k];
+        bag[k].m.src = (uint8_t)pi[s->msg[k].src]; bag[k].m.dst = (uint8_t)pi[s->msg[k].dst];
+        bag[k].cnt = s->cnt[k];
+    }
+    qsort(bag, (size_t)s->nmsg, sizeof bag[0], cmp_msg_cnt);
+    PUT(s->nmsg);
+    for (int k = 0; k < s->nmsg; k++) {
+        const Msg *m = &bag[k].m;
+        PUT(m->type); PUT(m->term); PUT(m->src << 4 | m->dst);
+        PUT(m->a); PUT(m->b); PUT(m->c); PUT(m->d); PUT(m->et); PUT(m->ev);
+        if (m->type == RVRESP || m->type == AEREQ) PUTLOG(m->mlog);
+        PUT(bag[k].cnt);
+    }
+    Elec el[EMAX];
+    for (int k = 0; k < s->nelec; k++) {
+        const Elec *e = &s->elec[k];
+        Elec *f = &el[k];
+        *f = *e;
+        f->leader = (uint8_t)pi[e->leader]; f->votes = perm_mask(e->votes, pi, N); f->vlp = perm_mask(e->vlp, pi, N);
+        memset(f->vl, 0, sizeof f->vl);
+        for (int j = 0; j < N; j++) f->vl[pi[j]] = e->vl[j];
+    }
+    qsort(el, (size_t)s->nelec, sizeof(Elec), (int (*)(const void *, const void *))elec_cmp);
+    PUT(s->nelec);
+    for (int k = 0; k < s->nelec; k++) {
+        const Elec *e = &el[k];
+        PUT(e->term); PUT(e->leader); PUT(e->votes); PUT(e->vlp);
+        PUTLOG(e->elog);
+        for (int j = 0; j < N; j++) if (e->vlp >> j & 1) PUTLOG(e->vl[j]);
+    }
+    PUT(s->nall & 255); PUT(s->nall >> 8);
+    for (int k = 0; k < s->nall; k++) PUTLOG(s->all[k]);
+#undef PUTLOG
+#undef PUT
+    return st;
+}
+
+/* Orderings sigma (position -> server) of the servers sorted by key[],
+ * permuting only within ties: sg_first starts them, sg_next advances (0
+ * after the last).  gb[0..ng] bound the tie groups. */
+static int sg_first(const int *key, int N, int *sg, int *gb) {
+    for (int i = 0; i < N; i++) sg[i] = i;
+    for (int i = 1; i < N; i++)       /* stable insertion sort by key */
+        for (int j = i; j > 0 && key[sg[j - 1]] > key[sg[j]]; j--) { int t = sg[j]; sg[j] = sg[j - 1]; sg[j - 1] = t; }
+    int ng = 0;
+    for (int p = 0; p < N; p++) if (!p || key[sg[p]] != key[sg[p - 1]]) gb[ng++] = p;
+    gb[ng] = N;
+    return ng;
+}
+static int sg_next(int *sg, const int *gb, int ng) {
+    int g = ng - 1;   /* an odometer over the tie groups' permutations */
+    while (g >= 0 && !next_perm(sg + gb[g], gb[g + 1] - gb[g])) {
+        /* (the group is in its last, descending order: back to ascending) */
+        for (int a = gb[g], b2 = gb[g + 1] - 1; a < b2; a++, b2--) { int t = sg[a]; sg[a] = sg[b2]; sg[b2] = t; }
+        g--;
+    }
+    return g >= 0;
+}
+
+/* serialise the orbit representative of s (the least orbit serialisation
+ * over all N! images) into out; returns its length.  Without SYMMETRY: the
+ * plain serialisation.  The least image begins with the N terms in
+ * ascending order, then within equal terms the roles ascending: every other
+ * image is above it in those first 2N bytes, so only the orderings of the
+ * servers tied on (term, role) are serialised and compared. */
 static size_t serialize_canon(const orc_cfg *c, const State *s, uint8_t *out) {
     const int N = c->n_server;
-    size_t best = serialize(c, s, out);
-    if (!c->symmetry) return best;
-    int pi[NMAX];
-    for (int i = 0; i < N; i++) pi[i] = i;
-    State *p = (State *)malloc(sizeof(State));
-    uint8_t *tmp = (uint8_t *)malloc(1 << 20);
-    for (;;) {  /* next permutation in lexicographic order */
-        int i = N - 2;
-        while (i >= 0 && pi[i] > pi[i + 1]) i--;
-        if (i < 0) break;
-        int j = N - 1;
-        while (pi[j] < pi[i]) j--;
-        int t = pi[i]; pi[i] = pi[j]; pi[j] = t;
-        for (int a = i + 1, b2 = N - 1; a < b2; a++, b2--) { t = pi[a]; pi[a] = pi[b2]; pi[b2] = t; }
-        permute_state(c, s, pi, p);
-        size_t len = serialize(c, p, tmp);
-        if (len != best) { g_spec_error = 1; break; }  /* impossible: same multiset of values */
-        if (memcmp(tmp, out, len) < 0) memcpy(out, tmp, len);
+    if (!c->symmetry) return serialize(c, s, out);
+    int key[NMAX] = {0}, sg[NMAX], gb[NMAX + 1], pi[NMAX];
+    for (int i = 0; i < N; i++) key[i] = s->s[i].term * 4 + s->s[i].role;
+    const int ng = sg_first(key, N, sg, gb);
+    static __thread uint8_t *scratch;   /* per worker thread, never freed */
+    if (!scratch) scratch = (uint8_t *)malloc(1 << 17);
+    uint8_t *tmp = scratch, *best = out;
+    const size_t len = serialize(c, s, tmp);   /* the orbit serialisation has the same length */
+    int first = 1;
+    do {
+        for (int p = 0; p < N; p++) pi[sg[p]] = p;
+        if (ser_image(c, s, pi, sg, first ? best : tmp, first ? NULL : best) < 0 && !first) {
+            uint8_t *t = best; best = tmp; tmp = t;
+        }
+        first = 0;
+    } while (sg_next(sg, gb, ng));
+    if (best != out) memcpy(out, best, len);
+    return len;
+}
+
+/* ------------------------------------------------------ orbit text digest -- */
+/* The digest of a SYMMETRY level is the sum of FNV-1a-64 of each orbit's
+ * ORBIT TEXT: the TLC text (state_text below) of the image pi(s) whose
+ * "rotated text" is least over all N! permutations, where the rotated text is
+ * the state text with its three lines that name no server function
+ * (messages, elections, allLogs) moved after the ten per-server lines.  It
+ * is a function of the orbit alone and is defined on TLC value text, so the
+ * product (rtla_level_orbit_hash, over its packed rows) and the value oracle
+ * (raft_values.orbit_text) compute it independently.  Here the per-server
+ * lines of each image are rendered with an early exit against the best so
+ * far; only images tying with it through them render their bag and elections. */
+typedef struct { char *p; size_t n; const char *best; size_t bn; int st; } RText;
+/* append t[0..k) comparing with best; returns 1 when the image is above best */
+static inline int rt_put(RText *r, const char *t, size_t k) {
+    if (r->st == 0) {
+        const size_t m = k < r->bn - r->n ? k : r->bn - r->n;
+        const int d = memcmp(t, r->best + r->n, m);
+        if (d > 0 || (d == 0 && m < k)) return 1;   /* (m < k: best ended first -- cannot happen) */
+        if (d < 0) r->st = -1;
     }
-    free(tmp); free(p);
-    return best;
+    memcpy(r->p + r->n, t, k);
+    r->n += k;
+    return 0;
+}
+static inline int rt_s(RText *r, const char *t) { return rt_put(r, t, strlen(t)); }
+static inline int rt_u(RText *r, unsigned v) {
+    char b[12]; int k = 0; char t[12];
+    do { t[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+    for (int i = 0; i < k; i++) b[i] = t[k - 1 - i];
+    return rt_put(r, b, (size_t)k);
+}
+static inline int rt_srv(RText *r, int j) { char b[3] = {'s', (char)('1' + j), 0}; return rt_put(r, b, 2); }
+static int rt_log(RText *r, Log l) {
+    const int n = log_len(l);
+    if (!n) return rt_s(r, "<<>>");
+    if (rt_s(r, "<<")) return 1;
+    for (int k = 1; k <= n; k++) {
+        if (k > 1 && rt_s(r, ", ")) return 1;
+        if (rt_s(r, "[term |-> ") || rt_u(r, (unsigned)log_term(l, k)) || rt_s(r, ", value |-> v") ||
+            rt_u(r, (unsigned)log_val(l, k) + 1) || rt_s(r, "]"))
+            return 1;
+    }
+    return rt_s(r, ">>");
+}
+static int rt_srvset(RText *r, int mask, int N) {
+    if (rt_s(r, "{")) return 1;
+    int first = 1;
+    for (int j = 0; j < N; j++)
+        if (mask >> j & 1) { if ((!first && rt_s(r, ", ")) || rt_srv(r, j)) return 1; first = 0; }
+    return rt_s(r, "}");
+}
+/* the per-server lines [from, 10) of the image pi(s) (sigma = pi^-1), each starting "\n" */
+static int rt_servers(const orc_cfg *c, const State *s, const int *pi, const int *sigma, RText *r, int from) {
+    const int N = c->n_server;
+    static const char *RN[3] = {"\"Follower\"", "\"Candidate\"", "\"Leader\""};
+    int ln = 0;
+#define LINE(name, body)                                                        \
+    if (ln++ >= from) {                                                         \
+        if (rt_s(r, "\n/\\ " name " = (")) return 1;                            \
+        for (int p = 0; p < N; p++) {                                           \
+            const Srv *v = &s->s[sigma[p]]; (void)v;                            \
+            if ((p && rt_s(r, " @@ ")) || rt_srv(r, p) || rt_s(r, " :> ")) return 1; \
+            body;                                                               \
+        }                                                                       \
+        if (rt_s(r, ")")) return 1;                                             \
+    }
+    LINE("currentTerm", if (rt_u(r, v->term)) return 1);
+    LINE("state", if (rt_s(r, RN[v->role])) return 1);
+    LINE("votedFor", if (v->voted == NIL ? rt_s(r, "\"Nil\"") : rt_srv(r, pi[v->voted])) return 1);
+    LINE("log", if (rt_log(r, v->log)) return 1);
+    LINE("commitIndex", if (rt_u(r, v->commit)) return 1);
+    LINE("votesResponded", if (rt_srvset(r, perm_mask(v->vresp, pi, N), N)) return 1);
+    LINE("votesGranted", if (rt_srvset(r, perm_mask(v->vgrant, pi, N), N)) return 1);
+    LINE("voterLog", {
+        const int vlp = perm_mask(v->vlp, pi, N);
+        if (!vlp) { if (rt_s(r, "<<>>")) return 1; }
+        else {
+            if (rt_s(r, "(")) return 1;
+            int first = 1;
+            for (int q = 0; q < N; q++)
+                if (vlp >> q & 1) {
+                    if ((!first && rt_s(r, " @@ ")) || rt_srv(r, q) || rt_s(r, " :> ") || rt_log(r, v->vl[sigma[q]]))
+                        return 1;
+                    first = 0;
+                }
+            if (rt_s(r, ")")) return 1;
+        }
+    });
+    LINE("nextIndex", {
+        if (rt_s(r, "(")) return 1;
+        for (int q = 0; q < N; q++)
+            if ((q && rt_s(r, " @@ ")) || rt_srv(r, q) || rt_s(r, " :> ") || rt_u(r, v->next[sigma[q]])) return 1;
+        if (rt_s(r, ")")) return 1;
+    });
+    LINE("matchIndex", {
+        if (rt_s(r, "(")) return 1;
+        for (int q = 0; q < N; q++)
+            if ((q && rt_s(r, " @@ ")) || rt_srv(r, q) || rt_s(r, " :> ") || rt_u(r, v->match[sigma[q]])) return 1;
+        if (rt_s(r, ")")) return 1;
+    });
+#undef LINE
+    return 0;
+}
+/* One message item "<record> :> count" of the image pi(s). */
+static void rt_msg(RText *r, const Msg *m, int cnt, const int *pi) {
+    static const char *TN[4] = {"RequestVoteRequest", "RequestVoteResponse", "AppendEntriesRequest",
+                                "AppendEntriesResponse"};
+    rt_s(r, "[mtype |-> \""); rt_s(r, TN[m->type]); rt_s(r, "\", mterm |-> "); rt_u(r, m->term); rt_s(r, ", ");
+    switch (m->type) {
+    case RVREQ:
+        rt_s(r, "mlastLogTerm |-> "); rt_u(r, m->a); rt_s(r, ", mlastLogIndex |-> "); rt_u(r, m->b); rt_s(r, ", ");
+        break;
+    case RVRESP:
+        rt_s(r, "mvoteGranted |-> "); rt_s(r, m->a ? "TRUE" : "FALSE"); rt_s(r, ", mlog |-> "); rt_log(r, m->mlog);
+        rt_s(r, ", ");
+        break;
+    case AEREQ:
+        rt_s(r, "mprevLogIndex |-> "); rt_u(r, m->a); rt_s(r, ", mprevLogTerm |-> "); rt_u(r, m->b);
+        rt_s(r, ", mentries |-> ");
+        if (m->d) { rt_s(r, "<<[term |-> "); rt_u(r, m->et); rt_s(r, ", value |-> v"); rt_u(r, m->ev + 1u); rt_s(r, "]>>"); }
+        else rt_s(r, "<<>>");
+        rt_s(r, ", mlog |-> "); rt_log(r, m->mlog); rt_s(r, ", mcommitIndex |-> "); rt_u(r, m->c); rt_s(r, ", ");
+        break;
+    default:
+        rt_s(r, "msuccess |-> "); rt_s(r, m->a ? "TRUE" : "FALSE"); rt_s(r, ", mmatchIndex |-> "); rt_u(r, m->b);
+        rt_s(r, ", ");
+    }
+    rt_s(r, "msource |-> "); rt_srv(r, pi[m->src]); rt_s(r, ", mdest |-> "); rt_srv(r, pi[m->dst]); rt_s(r, "]");
+    rt_s(r, " :> "); rt_u(r, (unsigned)cnt);
+}
+/* One election record of the image pi(s). */
+static void rt_elec(RText *r, const Elec *e, const int *pi, int N) {
+    rt_s(r, "[eterm |-> "); rt_u(r, e->term); rt_s(r, ", eleader |-> "); rt_srv(r, pi[e->leader]);
+    rt_s(r, ", elog |-> "); rt_log(r, e->elog); rt_s(r, ", evotes |-> "); rt_srvset(r, perm_mask(e->votes, pi, N), N);
+    rt_s(r, ", evoterLog |-> ");
+    const int vlp = perm_mask(e->vlp, pi, N);
+    if (!vlp) { rt_s(r, "<<>>"); }
+    else {
+        Log vl[NMAX];
+        for (int j = 0; j < N; j++) vl[pi[j]] = e->vl[j];
+        rt_s(r, "(");
+        int first = 1;
+        for (int q = 0; q < N; q++)
+            if (vlp >> q & 1) { if (!first) rt_s(r, " @@ "); rt_srv(r, q); rt_s(r, " :> "); rt_log(r, vl[q]); first = 0; }
+        rt_s(r, ")");
+    }
+    rt_s(r, "]");
+}
+typedef struct { const char *p; size_t n; } Item;
+static int item_cmp(const void *a, const void *b) {
+    const Item *x = (const Item *)a, *y = (const Item *)b;
+    const int d = memcmp(x->p, y->p, x->n < y->n ? x->n : y->n);
+    return d ? d : (x->n < y->n ? -1 : x->n > y->n);
+}
+/* "\n/\\ messages = ...\n/\\ elections = ..." of the image pi(s) into r
+ * (items rendered into `scratch`, sorted by text); 1 if above best */
+static int rt_bag(const orc_cfg *c, const State *s, const int *pi, RText *r, char *scratch) {
+    const int N = c->n_server;
+    Item it[KMAX > EMAX ? KMAX : EMAX];
+    RText w = {scratch, 0, NULL, 0, -1};
+    for (int k = 0; k < s->nmsg; k++) {
+        const size_t b = w.n;
+        rt_msg(&w, &s->msg[k], s->cnt[k], pi);
+        it[k].p = scratch + b; it[k].n = w.n - b;
+    }
+    qsort(it, (size_t)s->nmsg, sizeof(Item), item_cmp);
+    if (rt_s(r, "\n/\\ messages = ")) return 1;
+    if (!s->nmsg) { if (rt_s(r, "<<>>")) return 1; }
+    else {
+        if (rt_s(r, "(")) return 1;
+        for (int k = 0; k < s->nmsg; k++) if ((k && rt_s(r, " @@ ")) || rt_put(r, it[k].p, it[k].n)) return 1;
+        if (rt_s(r, ")")) return 1;
+    }
+    w.n = 0;
+    for (int k = 0; k < s->nelec; k++) {
+        const size_t b = w.n;
+        rt_elec(&w, &s->elec[k], pi, N);
+        it[k].p = scratch + b; it[k].n = w.n - b;
+    }
+    qsort(it, (size_t)s->nelec, sizeof(Item), item_cmp);
+    if (rt_s(r, "\n/\\ elections = ")) return 1;
+    if (!s->nelec) return rt_s(r, "{}");
+    if (rt_s(r, "{")) return 1;
+    for (int k = 0; k < s->nelec; k++) if ((k && rt_s(r, ", ")) || rt_put(r, it[k].p, it[k].n)) return 1;
+    return rt_s(r, "}");
+}
+static char *state_text(const orc_cfg *c, const State *s);
+/* The orbit text of s (malloc'd).  The rotated text of an image pi(s) is
+ * its ten per-server lines, then messages, elections (and allLogs, the same
+ * for every image: left out of the comparison).  Exact shortcut: the first
+ * two rotated lines (currentTerm, state) print one relabel-free token per
+ * position -- a decimal term, a quoted role, neither with a token a proper
+ * prefix of another that continues below the delimiters " @@ " / ")" -- so
+ * their least text puts the servers in (term text, role text) order and
+ * every image that does not is above it there; only the orderings of servers
+ * tied on (term, role) are compared, from the third line on.  (The value
+ * oracle, raft_values.orbit_text, compares all N! images in full.) */
+static char *orbit_text(const orc_cfg *c, const State *s) {
+    const int N = c->n_server;
+    static const int RRANK[3] = {1, 0, 2};   /* "Candidate" < "Follower" < "Leader" */
+    int key[NMAX], sg[NMAX], pi[NMAX], bpi[NMAX], gb[NMAX + 1];
+    for (int i = 0; i < N; i++) {
+        const int t = s->s[i].term;
+        key[i] = ((t >= 10 ? t / 10 : t) * 11 + (t >= 10 ? t % 10 + 1 : 0)) * 4 + RRANK[s->s[i].role];
+    }
+    const int ng = sg_first(key, N, sg, gb);
+    static __thread char *work;       /* two rotated texts + item scratch, per worker thread */
+    const size_t cap = 1 << 18;
+    if (!work) work = (char *)malloc(3 * cap);
+    char *bufs[2] = {work, work + cap}, *scratch = work + 2 * cap;
+    int bi = -1;
+    size_t bn = 0;
+    for (;;) {
+        for (int p = 0; p < N; p++) pi[sg[p]] = p;
+        const int ci = bi < 0 ? 0 : bi ^ 1;
+        RText q = {bufs[ci], 0, bi < 0 ? NULL : bufs[bi], bn, bi < 0 ? -1 : 0};
+        if (!rt_servers(c, s, pi, sg, &q, 2) && !rt_bag(c, s, pi, &q, scratch) && q.st < 0) {
+            bi = ci; bn = q.n;
+            memcpy(bpi, pi, sizeof pi);
+        }
+        if (!sg_next(sg, gb, ng)) break;
+    }
+    State *tmp = (State *)malloc(sizeof(State));
+    permute_state(c, s, bpi, tmp);
+    char *out = state_text(c, tmp);
+    free(tmp);
+    return out;
 }
 
 /* ------------------------------------------------------- text printing -- */
@@ -839,6 +1182,7 @@ typedef struct {
     uint64_t *text_hash; /* per thread */
     int count_only;      /* the last level of a max_levels prefix: count new states, keep none */
     uint64_t *nnew;      /* per thread: new states of the level */
+    uint64_t *max_bytes, *max_msgs;  /* per thread: largest new state (serialised bytes, bag slots) */
 } Bfs;
 
 typedef struct { Bfs *b; int tid; uint64_t parent_idx; uint8_t *ser; } EmitCtx;
@@ -864,11 +1208,14 @@ static void bfs_emit(void *ud, const State *t, int action, int arg) {
             b->nnew[e->tid]++;
             if (!b->count_only)
                 arena_push(&b->outs[e->tid], e->ser, len, e->parent_idx, (uint32_t)(action << 16 | arg));
-            if (b->check_text_hash) {
-                char *tx = state_text(b->c, t);
+            if (b->check_text_hash) {   /* SYMMETRY: the orbit text */
+                char *tx = b->c->symmetry ? orbit_text(b->c, t) : state_text(b->c, t);
                 b->text_hash[e->tid] += orc_text_hash(tx);
                 free(tx);
             }
+            /* (every new state, the count-only last level's included) */
+            if (len > b->max_bytes[e->tid]) b->max_bytes[e->tid] = len;
+            if ((uint64_t)t->nmsg > b->max_msgs[e->tid]) b->max_msgs[e->tid] = (uint64_t)t->nmsg;
         }
     }
     if (!inm || isnew) {
@@ -929,6 +1276,8 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
     b.cover = (uint64_t *)calloc((size_t)nthreads * A_COUNT, 8);
     b.text_hash = (uint64_t *)calloc((size_t)nthreads, 8);
     b.nnew = (uint64_t *)calloc((size_t)nthreads, 8);
+    b.max_bytes = (uint64_t *)calloc((size_t)nthreads, 8);
+    b.max_msgs = (uint64_t *)calloc((size_t)nthreads, 8);
 
     /* all levels (kept only when tracing) */
     Arena *levels = (Arena *)calloc(ORC_MAX_LEVELS + 1, sizeof(Arena));
@@ -943,7 +1292,12 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
     arena_push(&levels[0], ser, len, UINT64_MAX, 0);
     r->n_levels = 1;
     r->level_new[0] = 1; r->level_gen[0] = 1;
-    if (text_hash) { char *tx = state_text(c, s0); r->level_text_hash[0] = orc_text_hash(tx); free(tx); }
+    if (text_hash) {
+        char *tx = c->symmetry ? orbit_text(c, s0) : state_text(c, s0);
+        r->level_text_hash[0] = orc_text_hash(tx);
+        free(tx);
+    }
+    r->max_state_bytes = len;
     r->distinct = 1; r->generated = 1;
     int bad0 = check_inv(c, s0);
     int cur = 0;
@@ -983,11 +1337,9 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
             }
             arena_free(a);
         }
-        for (size_t q = 0; q < nx->cnt; q++) {
-            size_t l2 = (q + 1 < nx->cnt ? nx->off[q + 1] : nx->n) - nx->off[q];
-            if (l2 > r->max_state_bytes) r->max_state_bytes = l2;
-            int nm = nx->buf[nx->off[q]];
-            if ((uint64_t)nm > r->max_msgs) r->max_msgs = (uint64_t)nm;
+        for (int k = 0; k < nthreads; k++) {   /* (tracked per new state: the count-only level too) */
+            if (b.max_bytes[k] > r->max_state_bytes) r->max_state_bytes = b.max_bytes[k];
+            if (b.max_msgs[k] > r->max_msgs) r->max_msgs = b.max_msgs[k];
         }
         if (atomic_load(&b.viol)) { r->violated = atomic_load(&b.viol); rc = ORC_VIOLATION; }
         if (!keep_trace) { arena_free(&levels[cur]); }
@@ -1045,7 +1397,7 @@ int orc_bfs(const orc_cfg *c, int nthreads, int keep_trace, int text_hash, orc_r
     for (int L = 0; L <= cur && L <= ORC_MAX_LEVELS; L++) arena_free(&levels[L]);
     free(levels); free(level_base);
     for (int k = 0; k < nthreads; k++) arena_free(&b.outs[k]);
-    free(b.outs); free(b.gen); free(b.cover); free(b.text_hash); free(b.nnew);
+    free(b.outs); free(b.gen); free(b.cover); free(b.text_hash); free(b.nnew); free(b.max_bytes); free(b.max_msgs);
     free(b.v_state);
     seen_free(b.seen);
     free(s0); free(ser);
@@ -1133,3 +1485,317 @@ long orc_walk_text(void *h, char *buf, size_t cap) {
     return (long)l;
 }
 int orc_walk_inv(void *h) { Walk *w = (Walk *)h; return check_inv(&w->c, &w->cur); }
+
+/* SYMMETRY lockstep walks: the orbit text (see orbit_text) of each successor
+ * listed by the last orc_walk_successors, '\x1e'-separated, and the hex
+ * 128-bit hash of its least orbit serialisation (the oracle's seen-set key),
+ * as "hash\x1ftext\x1e".  Returns #successors or -needed bytes. */
+long orc_walk_orbits(void *h, char *buf, size_t cap) {
+    Walk *w = (Walk *)h;
+    Str o = {0};
+    sput(&o, "");
+    uint8_t *ser = (uint8_t *)malloc(1 << 17);
+    for (int k = 0; k < w->nsucc; k++) {
+        size_t len = serialize_canon(&w->c, &w->succ[k], ser);
+        uint64_t h1, h2;
+        hash128(ser, len, &h1, &h2);
+        sprintf_(&o, "%016llx%016llx\x1f", (unsigned long long)h1, (unsigned long long)h2);
+        char *tx = orbit_text(&w->c, &w->succ[k]);
+        sput(&o, tx); sput(&o, "\x1e");
+        free(tx);
+    }
+    free(ser);
+    long r = (long)w->nsucc;
+    if (o.n + 1 > cap) r = -(long)(o.n + 1);
+    else memcpy(buf, o.p, o.n + 1);
+    free(o.p);
+    return r;
+}
+
+/* ------------------------------------------- text parser + dedup (CPU leg) -- */
+/* The CPU baseline of the synthetic microbench (BASELINE configs[4]):
+ * arbitrary states given as TLC value text (the product's random rows, printed
+ * by rtla_random_texts) are parsed into this oracle's own representation and
+ * run through Next + dedup: generated successors, probes (in-model successors
+ * that differ from their parent) and distinct new successors, with the seen
+ * set kept across batches -- the counts the GPU's dedup kernel reports. */
+typedef struct { const char *p; int err; } Rd;
+static void rd_ex(Rd *q, const char *lit) {
+    const size_t n = strlen(lit);
+    if (strncmp(q->p, lit, n)) q->err = 1; else q->p += n;
+}
+static int rd_at(Rd *q, const char *lit) { return !strncmp(q->p, lit, strlen(lit)); }
+static int rd_int(Rd *q) {
+    if (*q->p < '0' || *q->p > '9') { q->err = 1; return 0; }
+    int v = 0;
+    while (*q->p >= '0' && *q->p <= '9') v = v * 10 + (*q->p++ - '0');
+    return v;
+}
+static int rd_srv(Rd *q) { rd_ex(q, "s"); return rd_int(q) - 1; }
+static int rd_bool(Rd *q) {
+    if (rd_at(q, "TRUE")) { q->p += 4; return 1; }
+    rd_ex(q, "FALSE");
+    return 0;
+}
+static Log rd_log(Rd *q) {
+    if (rd_at(q, "<<>>")) { q->p += 4; return 0; }
+    rd_ex(q, "<<");
+    Log l = 0;
+    for (int k = 0; !q->err && k < LCAP; k++) {
+        rd_ex(q, "[term |-> "); const int t = rd_int(q);
+        rd_ex(q, ", value |-> v"); const int v = rd_int(q) - 1;
+        rd_ex(q, "]");
+        l = log_append(l, t, v);
+        if (!rd_at(q, ", ")) break;
+        q->p += 2;
+    }
+    rd_ex(q, ">>");
+    return l;
+}
+static int rd_set(Rd *q) {
+    rd_ex(q, "{");
+    int m = 0;
+    if (!rd_at(q, "}"))
+        for (int k = 0; !q->err && k < NMAX; k++) {
+            m |= 1 << rd_srv(q);
+            if (!rd_at(q, ", ")) break;
+            q->p += 2;
+        }
+    rd_ex(q, "}");
+    return m;
+}
+static int rd_vl(Rd *q, Log *vl) {
+    if (rd_at(q, "<<>>")) { q->p += 4; return 0; }
+    rd_ex(q, "(");
+    int m = 0;
+    for (int k = 0; !q->err && k < NMAX; k++) {
+        const int j = rd_srv(q);
+        rd_ex(q, " :> ");
+        if (j < 0 || j >= NMAX) { q->err = 1; break; }
+        vl[j] = rd_log(q);
+        m |= 1 << j;
+        if (!rd_at(q, " @@ ")) break;
+        q->p += 4;
+    }
+    rd_ex(q, ")");
+    return m;
+}
+static void rd_msg(Rd *q, Msg *m, int *cnt) {
+    static const char *TN[4] = {"RequestVoteRequest\"", "RequestVoteResponse\"", "AppendEntriesRequest\"",
+                                "AppendEntriesResponse\""};
+    memset(m, 0, sizeof *m);
+    rd_ex(q, "[mtype |-> \"");
+    int t = 0;
+    while (t < 4 && !rd_at(q, TN[t])) t++;
+    if (t == 4) { q->err = 1; return; }
+    q->p += strlen(TN[t]);
+    m->type = (uint8_t)t;
+    rd_ex(q, ", mterm |-> "); m->term = (uint8_t)rd_int(q); rd_ex(q, ", ");
+    switch (t) {
+    case RVREQ:
+        rd_ex(q, "mlastLogTerm |-> "); m->a = (uint8_t)rd_int(q);
+        rd_ex(q, ", mlastLogIndex |-> "); m->b = (uint8_t)rd_int(q);
+        break;
+    case RVRESP:
+        rd_ex(q, "mvoteGranted |-> "); m->a = (uint8_t)rd_bool(q);
+        rd_ex(q, ", mlog |-> "); m->mlog = rd_log(q);
+        break;
+    case AEREQ:
+        rd_ex(q, "mprevLogIndex |-> "); m->a = (uint8_t)rd_int(q);
+        rd_ex(q, ", mprevLogTerm |-> "); m->b = (uint8_t)rd_int(q);
+        rd_ex(q, ", mentries |-> ");
+        if (rd_at(q, "<<>>")) { q->p += 4; }
+        else {
+            rd_ex(q, "<<[term |-> "); m->et = (uint8_t)rd_int(q);
+            rd_ex(q, ", value |-> v"); m->ev = (uint8_t)(rd_int(q) - 1);
+            rd_ex(q, "]>>"); m->d = 1;
+        }
+        rd_ex(q, ", mlog |-> "); m->mlog = rd_log(q);
+        rd_ex(q, ", mcommitIndex |-> "); m->c = (uint8_t)rd_int(q);
+        break;
+    default:
+        rd_ex(q, "msuccess |-> "); m->a = (uint8_t)rd_bool(q);
+        rd_ex(q, ", mmatchIndex |-> "); m->b = (uint8_t)rd_int(q);
+    }
+    rd_ex(q, ", msource |-> "); m->src = (uint8_t)rd_srv(q);
+    rd_ex(q, ", mdest |-> "); m->dst = (uint8_t)rd_srv(q);
+    rd_ex(q, "] :> "); *cnt = rd_int(q);
+}
+/* Parse one state text (state_text's format) into s; 0 on success. */
+static int parse_state(const orc_cfg *c, const char *text, State *s) {
+    const int N = c->n_server;
+    Rd q = {text, 0};
+    memset(s, 0, sizeof *s);
+    rd_ex(&q, "/\\ messages = ");
+    if (rd_at(&q, "<<>>")) q.p += 4;
+    else {
+        rd_ex(&q, "(");
+        while (!q.err) {
+            Msg m; int cnt = 0, pos;
+            rd_msg(&q, &m, &cnt);
+            if (q.err || m.src >= N || m.dst >= N || cnt < 1 || s->nmsg >= KMAX || bag_find(s, &m, &pos)) return -1;
+            memmove(&s->msg[pos + 1], &s->msg[pos], sizeof(Msg) * (s->nmsg - pos));
+            memmove(&s->cnt[pos + 1], &s->cnt[pos], s->nmsg - pos);
+            s->msg[pos] = m; s->cnt[pos] = (uint8_t)cnt; s->nmsg++;
+            if (!rd_at(&q, " @@ ")) break;
+            q.p += 4;
+        }
+        rd_ex(&q, ")");
+    }
+    rd_ex(&q, "\n/\\ elections = {");
+    if (!rd_at(&q, "}"))
+        while (!q.err) {
+            Elec e; memset(&e, 0, sizeof e);
+            rd_ex(&q, "[eterm |-> "); e.term = (uint8_t)rd_int(&q);
+            rd_ex(&q, ", eleader |-> "); e.leader = (uint8_t)rd_srv(&q);
+            rd_ex(&q, ", elog |-> "); e.elog = rd_log(&q);
+            rd_ex(&q, ", evotes |-> "); e.votes = (uint8_t)rd_set(&q);
+            rd_ex(&q, ", evoterLog |-> "); e.vlp = (uint8_t)rd_vl(&q, e.vl);
+            rd_ex(&q, "]");
+            if (q.err || s->nelec >= EMAX) return -1;
+            elec_add(s, &e);
+            if (!rd_at(&q, ", ")) break;
+            q.p += 2;
+        }
+    rd_ex(&q, "}\n/\\ allLogs = {");
+    if (!rd_at(&q, "}"))
+        while (!q.err) {
+            all_add(s, rd_log(&q));
+            if (!rd_at(&q, ", ")) break;
+            q.p += 2;
+        }
+    rd_ex(&q, "}");
+    static const char *NAME[10] = {"currentTerm", "state", "votedFor", "log", "commitIndex", "votesResponded",
+                                   "votesGranted", "voterLog", "nextIndex", "matchIndex"};
+    for (int k = 0; k < 10 && !q.err; k++) {
+        rd_ex(&q, "\n/\\ "); rd_ex(&q, NAME[k]); rd_ex(&q, " = (");
+        for (int i = 0; i < N && !q.err; i++) {
+            Srv *v = &s->s[i];
+            if (i) rd_ex(&q, " @@ ");
+            if (rd_srv(&q) != i) return -1;
+            rd_ex(&q, " :> ");
+            switch (k) {
+            case 0: v->term = (uint8_t)rd_int(&q); break;
+            case 1:
+                if (rd_at(&q, "\"Follower\"")) { v->role = FOLLOWER; q.p += 10; }
+                else if (rd_at(&q, "\"Candidate\"")) { v->role = CANDIDATE; q.p += 11; }
+                else { rd_ex(&q, "\"Leader\""); v->role = LEADER; }
+                break;
+            case 2:
+                if (rd_at(&q, "\"Nil\"")) { v->voted = NIL; q.p += 5; }
+                else v->voted = (uint8_t)rd_srv(&q);
+                break;
+            case 3: v->log = rd_log(&q); break;
+            case 4: v->commit = (uint8_t)rd_int(&q); break;
+            case 5: v->vresp = (uint8_t)rd_set(&q); break;
+            case 6: v->vgrant = (uint8_t)rd_set(&q); break;
+            case 7: v->vlp = (uint8_t)rd_vl(&q, v->vl); break;
+            default:
+                rd_ex(&q, "(");
+                for (int j = 0; j < N && !q.err; j++) {
+                    if (j) rd_ex(&q, " @@ ");
+                    if (rd_srv(&q) != j) return -1;
+                    rd_ex(&q, " :> ");
+                    if (k == 8) v->next[j] = (uint8_t)rd_int(&q); else v->match[j] = (uint8_t)rd_int(&q);
+                }
+                rd_ex(&q, ")");
+            }
+        }
+        rd_ex(&q, ")");
+    }
+    return q.err || *q.p ? -1 : 0;
+}
+
+typedef struct {
+    orc_cfg c;
+    SeenSet *seen;
+    uint64_t gen, probes, nnew;
+} Dedup;
+typedef struct {
+    Dedup *d;
+    const char *const *texts;
+    size_t n;
+    atomic_size_t next;
+    atomic_int err;
+    uint64_t *cnt;   /* per thread: gen, probes, new */
+    int tid_next;
+    pthread_mutex_t mu;
+} DedupJob;
+typedef struct { DedupJob *j; int tid; uint8_t *pser; size_t plen; uint8_t *ser; } DedupEmit;
+static void dedup_emit(void *ud, const State *t, int action, int arg) {
+    (void)action; (void)arg;
+    DedupEmit *e = (DedupEmit *)ud;
+    uint64_t *cnt = e->j->cnt + 3 * e->tid;
+    cnt[0]++;
+    if (!in_model(&e->j->d->c, t)) return;
+    const size_t len = serialize(&e->j->d->c, t, e->ser);
+    if (len == e->plen && !memcmp(e->ser, e->pser, len)) return;   /* the parent itself */
+    cnt[1]++;
+    uint64_t h1, h2;
+    hash128(e->ser, len, &h1, &h2);
+    cnt[2] += (uint64_t)seen_put(e->j->d->seen, h1, h2);
+}
+static void *dedup_worker(void *arg) {
+    DedupJob *j = (DedupJob *)arg;
+    pthread_mutex_lock(&j->mu);
+    DedupEmit e = {j, j->tid_next++, NULL, 0, NULL};
+    pthread_mutex_unlock(&j->mu);
+    State *s = (State *)malloc(sizeof(State)), *t = (State *)malloc(sizeof(State)), *base = (State *)malloc(sizeof(State));
+    e.pser = (uint8_t *)malloc(1 << 17);
+    e.ser = (uint8_t *)malloc(1 << 17);
+    for (;;) {
+        const size_t i = atomic_fetch_add(&j->next, 1);
+        if (i >= j->n) break;
+        if (parse_state(&j->d->c, j->texts[i], s)) { atomic_store(&j->err, 1); break; }
+        e.plen = serialize(&j->d->c, s, e.pser);
+        expand(&j->d->c, s, base, t, dedup_emit, &e);
+    }
+    free(s); free(t); free(base); free(e.pser); free(e.ser);
+    return NULL;
+}
+void *orc_dedup_new(const orc_cfg *c) {
+    Dedup *d = (Dedup *)calloc(1, sizeof(Dedup));
+    d->c = *c;
+    d->seen = seen_new();
+    return d;
+}
+void orc_dedup_free(void *h) {
+    Dedup *d = (Dedup *)h;
+    if (!d) return;
+    seen_free(d->seen);
+    free(d);
+}
+/* Expand + dedup the states of `texts` ('\x1e'-terminated state texts, n of
+ * them), threads workers; out[0..2] += generated, probes, new; out[3] =
+ * seconds of this call.  Returns 0, or -1 on a text it cannot parse. */
+int orc_dedup_texts(void *h, const char *texts, size_t n, int threads, uint64_t *out, double *seconds) {
+    Dedup *d = (Dedup *)h;
+    g_overflow = 0; g_spec_error = 0;
+    const char **v = (const char **)malloc(sizeof(char *) * (n ? n : 1));
+    char *buf = strdup(texts);
+    char *p = buf;
+    for (size_t i = 0; i < n; i++) {
+        v[i] = p;
+        char *e = strchr(p, '\x1e');
+        if (!e) { free(v); free(buf); return -1; }
+        *e = 0;
+        p = e + 1;
+    }
+    if (threads < 1) threads = 1;
+    DedupJob j;
+    memset(&j, 0, sizeof j);
+    j.d = d; j.texts = v; j.n = n;
+    atomic_store(&j.next, 0); atomic_store(&j.err, 0);
+    j.cnt = (uint64_t *)calloc((size_t)threads * 3, 8);
+    pthread_mutex_init(&j.mu, NULL);
+    const double t0 = now_s();
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    for (int k = 0; k < threads; k++) pthread_create(&th[k], NULL, dedup_worker, &j);
+    for (int k = 0; k < threads; k++) pthread_join(th[k], NULL);
+    if (seconds) *seconds = now_s() - t0;
+    for (int k = 0; k < threads; k++)
+        for (int x = 0; x < 3; x++) out[x] += j.cnt[3 * k + x];
+    free(th); free(j.cnt); free(v); free(buf);
+    pthread_mutex_destroy(&j.mu);
+    return atomic_load(&j.err) || g_overflow || g_spec_error ? -1 : 0;
+}

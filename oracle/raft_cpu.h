@@ -33,7 +33,8 @@ typedef struct {
     uint64_t distinct, generated;
     uint64_t level_new[ORC_MAX_LEVELS];
     uint64_t level_gen[ORC_MAX_LEVELS];
-    uint64_t level_text_hash[ORC_MAX_LEVELS];  /* sum of FNV-1a(text) over new states */
+    uint64_t level_text_hash[ORC_MAX_LEVELS];  /* sum of FNV-1a(text) over new states; SYMMETRY:
+                                                  of each new orbit's orbit text (raft_cpu.c) */
     uint64_t coverage[ORC_MAX_ACTIONS];
     uint64_t max_msgs, max_state_bytes;
     double seconds;
@@ -50,6 +51,11 @@ long orc_walk_successors(void *h, char *buf, size_t cap);
 int orc_walk_goto(void *h, const char *text);
 long orc_walk_text(void *h, char *buf, size_t cap);
 int orc_walk_inv(void *h);
+long orc_walk_orbits(void *h, char *buf, size_t cap);
+
+void *orc_dedup_new(const orc_cfg *c);
+void orc_dedup_free(void *h);
+int orc_dedup_texts(void *h, const char *texts, size_t n, int threads, uint64_t *out, double *seconds);
 
 #ifdef __cplusplus
 }

@@ -59,6 +59,13 @@ def lib():
         _lib.orc_walk_text.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
         _lib.orc_walk_text.restype = C.c_long
         _lib.orc_walk_inv.argtypes = [C.c_void_p]
+        _lib.orc_walk_orbits.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        _lib.orc_walk_orbits.restype = C.c_long
+        _lib.orc_dedup_new.argtypes = [C.POINTER(OrcCfg)]
+        _lib.orc_dedup_new.restype = C.c_void_p
+        _lib.orc_dedup_free.argtypes = [C.c_void_p]
+        _lib.orc_dedup_texts.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_int, C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_double)]
     return _lib
 
 
@@ -112,6 +119,20 @@ class Walk:
         items = [x for x in buf.raw[:buf.raw.index(b"\0")].decode().split("\x1e") if x]
         return [(it[0] == "1", it[2:]) for it in items]
 
+    def orbits(self):
+        """SYMMETRY: for each successor of the last successors() call, its
+        oracle seen-set key (hash of the least orbit serialisation, hex) and
+        its orbit text."""
+        cap = 1 << 20
+        while True:
+            buf = C.create_string_buffer(cap)
+            n = lib().orc_walk_orbits(self.h, buf, cap)
+            if n >= 0:
+                break
+            cap = -n + 16
+        items = [x for x in buf.raw[:buf.raw.index(b"\0")].decode().split("\x1e") if x]
+        return [tuple(it.split("\x1f", 1)) for it in items]
+
     def goto(self, text: str):
         if lib().orc_walk_goto(self.h, text.encode()) != 0:
             raise KeyError("successor not found")
@@ -127,6 +148,34 @@ class Walk:
     def close(self):
         if self.h:
             lib().orc_walk_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class Dedup:
+    """Next + dedup of arbitrary states given as state texts (the synthetic
+    microbench's CPU leg): counts (generated, probes, new) accumulate over
+    batches that share one seen set."""
+
+    def __init__(self, cfg: OrcCfg):
+        self.h = lib().orc_dedup_new(C.byref(cfg))
+        self.counts = [0, 0, 0]
+        self.seconds = 0.0
+
+    def batch(self, texts: bytes, n: int, threads: int = 8):
+        out = (C.c_uint64 * 3)(*self.counts)
+        sec = C.c_double(0)
+        if lib().orc_dedup_texts(self.h, texts, n, threads, out, C.byref(sec)) != 0:
+            raise RuntimeError("oracle dedup: unparsable state text or capacity overflow")
+        self.counts = list(out)
+        self.seconds += sec.value
+        return self.counts
+
+    def close(self):
+        if self.h:
+            lib().orc_dedup_free(self.h)
             self.h = None
 
     def __del__(self):

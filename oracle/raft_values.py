@@ -22,7 +22,7 @@ Every action cites the raft.tla line it transcribes.  The model-checking
 wrapper (state constraint and invariants) is NOT part of the reference
 (``raft.cfg:3`` names an undefined ``NoTwoLeaders`` and there is no
 CONSTRAINT); the definitions used here are the build's own and are recorded
-verbatim in ``oracle/MC.tla`` and DESIGN.md.
+verbatim in ``specs/MC.tla`` and DESIGN.md.
 
 Parity status: TLC (the reference's engine) cannot run in this container or on
 the GPU box (no JVM), and the reference ships no tests or fixtures, so this
@@ -484,7 +484,7 @@ def next_states(cfg: Cfg, s: tuple) -> List[Tuple[str, tuple]]:
 
 
 # -------------------------------------------- build-defined MC wrapper ----
-# Recorded verbatim in oracle/MC.tla.  NOT part of the reference.
+# Recorded verbatim in specs/MC.tla.  NOT part of the reference.
 
 def in_model(cfg: Cfg, s: tuple) -> bool:
     """StateConstraint == /\\ \\A i \\in Server : currentTerm[i] <= MaxTerm
@@ -669,13 +669,34 @@ def orbit_key(cfg: Cfg, s: tuple) -> str:
     return min(state_text(cfg, permute_state(s, pi)) for pi in itertools.permutations(range(cfg.n_server)))
 
 
-def bfs_symmetric(cfg: Cfg) -> List[Tuple[int, int]]:
+def rotated_text(cfg: Cfg, s: tuple) -> str:
+    """The state text with its three lines that are no function on Server
+    (messages, elections, allLogs) moved after the ten per-server lines."""
+    lines = state_text(cfg, s).split("\n")
+    return "\n".join(lines[3:] + lines[:3])
+
+
+def orbit_text(cfg: Cfg, s: tuple) -> str:
+    """The orbit text of s: the state text of the image whose rotated text is
+    least over all server permutations -- a function of the orbit alone, the
+    per-orbit item of a SYMMETRY level's digest (oracle/raft_cpu.c orbit_text,
+    the product's rtla_level_orbit_hash).  Brute force over every image."""
+    import itertools
+    imgs = (permute_state(s, pi) for pi in itertools.permutations(range(cfg.n_server)))
+    return state_text(cfg, min(imgs, key=lambda t: rotated_text(cfg, t)))
+
+
+def bfs_symmetric(cfg: Cfg, orbit_hashes: Optional[List[int]] = None) -> List[Tuple[int, int]]:
     """Per-level (new orbits, generated) of the BFS under SYMMETRY
     Permutations(Server): a successor is new iff no state of its orbit was
-    seen; the state itself (not a representative) is explored, as in TLC."""
+    seen; the state itself (not a representative) is explored, as in TLC.
+    orbit_hashes (a list) receives each level's digest: the sum mod 2^64 of
+    FNV-1a(orbit_text) over its new orbits."""
     s0 = init_state(cfg)
     seen = {orbit_key(cfg, s0)}
     levels, frontier = [(1, 1)], [s0]
+    if orbit_hashes is not None:
+        orbit_hashes.append(fnv1a64(orbit_text(cfg, s0)))
     while frontier:
         nxt, gen = [], 0
         for s in frontier:
@@ -687,6 +708,8 @@ def bfs_symmetric(cfg: Cfg) -> List[Tuple[int, int]]:
                         seen.add(k)
                         nxt.append(t)
         levels.append((len(nxt), gen))
+        if orbit_hashes is not None:
+            orbit_hashes.append(sum(fnv1a64(orbit_text(cfg, t)) for t in nxt) & 0xFFFFFFFFFFFFFFFF)
         frontier = nxt
     return levels
 

@@ -57,6 +57,7 @@ RTLA_HD unsigned long long ring_idx(const Ring& r, unsigned long long g) {
 struct ShardBox {
   int nshard, me;
   unsigned long long cap;
+  int slog2;                      // log2 slots of the sent cache (MULTI)
   unsigned long long* out_count;  // [nshard]
   unsigned long long* send_fp;    // [nshard][cap][2]
   unsigned long long* send_ref;   // [nshard][cap]: local parent index << 16 | instance

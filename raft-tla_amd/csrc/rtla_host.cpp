@@ -88,13 +88,14 @@ struct Shard {
   uint64_t* recv_fp = nullptr;     // [G][cap][2]
   uint32_t* recv_ans = nullptr;    // [G][cap]  our answers to the senders
   uint64_t* new_count = nullptr;   // [G] device: new fingerprints we own, per source
-  uint64_t* all_new = nullptr;     // [G][G] device (RCCL all-gather target)
-  uint64_t* rows_in = nullptr;     // [G] device: rows received per source (this sub-round)
+  uint64_t* all_new = nullptr;     // [G][G] device (unused since the two-phase exchange)
+  uint64_t* rows_in = nullptr;     // [G] device: rows received per source (re-balancing sub-round)
   uint64_t* rows_base = nullptr;   // [G] device: next-frontier slot of each source's first row
-  uint32_t* send_rows = nullptr;   // [G][rows_cap][W + 2]
+  uint32_t* send_rows = nullptr;   // [G][rows_cap][W + 2]  re-balancing staging
   uint32_t* recv_rows = nullptr;   // [G][rows_cap][W + 2]
-  uint64_t* sent = nullptr;        // [2^tlog2] fingerprints this shard already sent to their owners
-  std::vector<uint64_t> h_out, h_in, h_new_out, h_new_in, h_all;
+  uint64_t* sent = nullptr;        // [2^slog2] sent cache: fingerprints this shard already sent to their owners
+  std::vector<uint64_t> h_out, h_in, h_all;
+  uint64_t h_reb[2 * SHARD_MAX] = {};  // re-balancing: rows_in / rows_base of this sub-round (host staging)
   uint64_t h_caps[3] = {0, 0, 0};  // -> DevCounters cap_cur / cap_next / cap_parents
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   // violation found on this shard
@@ -133,7 +134,9 @@ struct rtla_ctx {
   ShmComm* shm = nullptr;  // RTLA_TRANSPORT=shm instead of RCCL
   bool rccl_local = false; // world 1, S shards, RTLA_TRANSPORT=rccl: the exchange goes through `comm` (1 rank)
   int tlog2 = 0;
+  int slog2 = 0;           // sent cache: 2^slog2 slots per shard (multi-shard)
   uint64_t front_cap = 0, box_cap = 0, chunk = 0, rows_cap = 0;
+  uint64_t rebalanced = 0; // rows moved by level-end re-balancing (all levels, this process's shards)
   uint64_t* red = nullptr;  // device scratch for all-reduces
   int level = 0;
   bool inited = false, finished = false;
@@ -515,7 +518,7 @@ static uint64_t fnv1a64_sum(char* const* txt, const size_t* len, int m) {
   return sum;
 }
 
-static uint64_t rows_digest(const Layout& L, const uint32_t* rows, size_t n, int threads) {
+static uint64_t rows_digest(const Layout& L, const uint32_t* rows, size_t n, int threads, bool orbit = false) {
   threads = (int)std::min<size_t>((size_t)threads, std::max<size_t>(1, n / 4096));
   std::vector<uint64_t> part((size_t)threads, 0);
   std::atomic<size_t> next{0};
@@ -533,7 +536,9 @@ static uint64_t rows_digest(const Layout& L, const uint32_t* rows, size_t n, int
       const size_t e = std::min(n, b + 8192);
       for (size_t k = b; k < e; k += TEXT_ILP) {
         const int m = (int)std::min<size_t>(TEXT_ILP, e - k);
-        for (int i = 0; i < m; i++) len[i] = state_text_into(L, rows + (k + i) * (size_t)L.W, txt[i], scratch);
+        for (int i = 0; i < m; i++)
+          len[i] = orbit ? state_orbit_text_into(L, rows + (k + i) * (size_t)L.W, txt[i], scratch)
+                         : state_text_into(L, rows + (k + i) * (size_t)L.W, txt[i], scratch);
         acc += fnv1a64_sum(txt, len, m);
       }
     }
@@ -555,6 +560,28 @@ extern "C" int rtla_rows_text_hash(const rtla_cfg* c, const uint32_t* rows, size
   if (!out || (n && !rows)) return RTLA_E_ARG;
   *out = rows_digest(L, rows, n, text_threads(threads));
   return RTLA_OK;
+}
+
+extern "C" int rtla_rows_orbit_hash(const rtla_cfg* c, const uint32_t* rows, size_t n, int threads, uint64_t* out) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  if (!out || (n && !rows)) return RTLA_E_ARG;
+  *out = rows_digest(L, rows, n, text_threads(threads), true);
+  return RTLA_OK;
+}
+
+extern "C" int rtla_orbit_text(const rtla_cfg* c, const uint32_t* row, char* buf, size_t cap) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  const size_t tc = state_text_cap(L);
+  std::vector<char> b(2 * tc);
+  const size_t n = state_orbit_text_into(L, row, b.data(), b.data() + tc);
+  if (n + 1 > cap) return RTLA_E_ARG;
+  memcpy(buf, b.data(), n);
+  buf[n] = 0;
+  return (int)n;
 }
 
 static int flags_to_status(int flags) {
@@ -604,7 +631,7 @@ static int expand_batch_dev(const Layout& L, const uint32_t* d_rows, size_t n, s
     const uint64_t caps[3] = {round64(n), cap, cap};  // DevCounters cap_cur / cap_next / cap_parents
     HIPCHK(hipMemcpyAsync(&d_ctr->cap_cur, caps, sizeof caps, hipMemcpyHostToDevice, st));
     const Ring cur{const_cast<uint32_t*>(d_rows), 0, round64(n)}, next{d_out, 0, cap};
-    ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+    ShardBox box{1, 0, 0, 0, nullptr, nullptr, nullptr};
     HIPCHK(launch_expand(L, cur, 0, n, 0, next, d_info, 0, cap, nullptr, 1, d_ctr, box, 0, st,
                          XF_ALL_SUCCESSORS | XF_NO_COVER, nullptr));
   } else {
@@ -673,6 +700,41 @@ extern "C" int rtla_random_rows(const rtla_cfg* c, uint64_t seed, uint64_t first
   return RTLA_OK;
 }
 
+extern "C" int rtla_random_texts(const rtla_cfg* c, uint64_t seed, uint64_t first, uint64_t n, uint64_t pool,
+                                 char* buf, size_t cap, size_t* len) {
+  Layout L;
+  int r = layout_from_cfg(c, &L);
+  if (r) return r;
+  if (!len || (!buf && cap)) return RTLA_E_ARG;
+  // host threads, each rendering a contiguous slice of the inputs
+  const int nt = (int)std::min<uint64_t>(std::max<uint64_t>(n / 256, 1), (uint64_t)text_threads(0));
+  std::vector<std::string> part((size_t)nt);
+  auto work = [&](int t) {
+    const size_t tc = state_text_cap(L);
+    std::vector<uint32_t> row(L.W);
+    std::vector<char> tmp(2 * tc);
+    const uint64_t b = n * t / nt, e = n * (t + 1) / nt;
+    std::string& out = part[(size_t)t];
+    for (uint64_t k = b; k < e; k++) {
+      random_state(L, seed, synth_state_id(seed, first + k, pool), row.data());
+      const size_t m = state_text_into(L, row.data(), tmp.data(), tmp.data() + tc);
+      out.append(tmp.data(), m);
+      out.push_back('\x1e');
+    }
+  };
+  std::vector<std::thread> pool_th;
+  for (int t = 1; t < nt; t++) pool_th.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool_th) th.join();
+  size_t at = 0;
+  for (auto& p : part) {
+    if (at + p.size() <= cap) memcpy(buf + at, p.data(), p.size());
+    at += p.size();
+  }
+  *len = at;
+  return at <= cap ? RTLA_OK : RTLA_E_ARG;
+}
+
 extern "C" int rtla_comm_id(void* out128) {
   if (!out128) return RTLA_E_ARG;
   const char* tr = getenv("RTLA_TRANSPORT");
@@ -731,8 +793,9 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   uint64_t boxb = G > 1 ? (uint64_t)G * x->box_cap * (16 + 8 + 4 + 16 + 4) +
                               2ull * G * x->rows_cap * (L.W + 2) * 4
                         : 0;
+  const uint64_t sbytes = G > 1 ? 8ull << x->slog2 : 0;
   if (!x->front_cap) {
-    uint64_t used = tbytes * (G > 1 ? 2 : 1) + pbytes + boxb;
+    uint64_t used = tbytes + sbytes + pbytes + boxb;
     uint64_t rest = budget > used ? budget - used : 0;
     x->front_cap = std::max<uint64_t>(rest / rowb, 2048);
   }
@@ -759,11 +822,9 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
     HIPCHK(hipMalloc(&s.recv_rows, 4ull * G * x->rows_cap * (L.W + 2)));
     s.h_out.assign(G, 0);
     s.h_in.assign(G, 0);
-    s.h_new_out.assign(G, 0);
-    s.h_new_in.assign(G, 0);
     s.h_all.assign((size_t)G * G, 0);
-    HIPCHK(hipMalloc(&s.sent, tbytes));
-    HIPCHK(hipMemsetAsync(s.sent, 0, tbytes, x->stream));
+    HIPCHK(hipMalloc(&s.sent, sbytes));
+    HIPCHK(hipMemsetAsync(s.sent, 0, sbytes, x->stream));
   }
   HIPCHK(hipMemsetAsync(s.table, 0, tbytes, x->stream));
   HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
@@ -841,19 +902,22 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
     }
     x->chunk = round64(x->chunk);  // exchange rounds start at 64-row group boundaries (Ring)
     x->box_cap = x->chunk * nmax;
-    // row regions: ~1/10 of the budget; winners beyond it ship in sub-rounds
-    x->rows_cap = (per / 10) / (2ull * G * (L.W + 2) * 4);
+    // re-balancing staging: ~1/20 of the budget; more rows move in sub-rounds
+    x->rows_cap = (per / 20) / (2ull * G * (L.W + 2) * 4);
     x->rows_cap = std::min<uint64_t>(std::max<uint64_t>(x->rows_cap, 256), x->box_cap);
   }
   int tl = cfg->fpset_log2;
   if (!tl) {
     tl = 20;
-    // the fingerprint set (and, multi-shard, the equally sized sent cache): ~40% of the budget
-    const uint64_t tshare = G > 1 ? per / 5 : per * 2 / 5;
+    // the fingerprint set (multi-shard: + the sent cache, a quarter of its size): ~40% of the budget
+    const uint64_t tshare = G > 1 ? per * 8 / 25 : per * 2 / 5;
     while (tl < 34 && (8ull << (tl + 1)) <= tshare) tl++;
   }
   if (tl < 10 || tl > 40) { rtla_close(x); return RTLA_E_CONFIG; }
   x->tlog2 = tl;
+  // the sent cache is a dedup hint (one slot per fingerprint, overwritten on
+  // a miss): a quarter of the set's slots
+  x->slog2 = std::max(12, tl - 2);
   x->front_cap = cfg->frontier_cap;
   x->sh.resize(nlocal);
   for (int k = 0; k < nlocal; k++) {
@@ -883,10 +947,11 @@ extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
   snprintf(buf, cap,
            "{\"device\": \"%s\", \"arch\": \"%s\", \"cus\": %d, \"rank\": %d, \"world\": %d, \"shards\": %d, "
            "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu, "
-           "\"transport\": \"%s\"}",
+           "\"transport\": \"%s\", \"sent_cache_slots_log2\": %d, \"rebalanced_rows\": %llu}",
            p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
            (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk,
-           x->shm ? "shm" : x->comm ? (x->rccl_local ? "rccl-local" : "rccl") : "device");
+           x->shm ? "shm" : x->comm ? (x->rccl_local ? "rccl-local" : "rccl") : "device", x->nshard > 1 ? x->slog2 : 0,
+           (unsigned long long)x->rebalanced);
   return RTLA_OK;
 }
 
@@ -995,7 +1060,7 @@ extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
     if (!f) { failed = 1; break; }
     DevCounters c;
     bool ok = write_all(f, &h, sizeof h) && dev_to_file(f, s.table, 8ull << x->tlog2, buf) &&
-              (!s.sent || dev_to_file(f, s.sent, 8ull << x->tlog2, buf)) &&
+              (!s.sent || dev_to_file(f, s.sent, 8ull << x->slog2, buf)) &&
               dev_to_file(f, s.parents, 8 * h.parents_n, buf) &&
               ring_to_file(f, cur_ring(x, s), x->L.W, s.n_cur, buf) &&
               hipMemcpy(&c, s.ctr, sizeof c, hipMemcpyDeviceToHost) == hipSuccess &&
@@ -1041,7 +1106,7 @@ extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
     DevCounters c;
     memset(&c, 0, sizeof c);
     ok = ok && file_to_dev(f, s.table, 8ull << x->tlog2, buf) &&
-         (!s.sent || file_to_dev(f, s.sent, 8ull << x->tlog2, buf)) &&
+         (!s.sent || file_to_dev(f, s.sent, 8ull << x->slog2, buf)) &&
          file_to_dev(f, s.parents, 8 * h.parents_n, buf) &&
          file_to_dev(f, s.arena, 4ull * x->L.W * h.n_cur, buf) && read_all(f, c.cover, sizeof c.cover);
     fclose(f);
@@ -1081,7 +1146,7 @@ extern "C" int rtla_reset(rtla_ctx* x) {
   HIPCHK(hipSetDevice(x->device));
   for (auto& s : x->sh) {
     HIPCHK(hipMemsetAsync(s.table, 0, 8ull << x->tlog2, x->stream));
-    if (s.sent) HIPCHK(hipMemsetAsync(s.sent, 0, 8ull << x->tlog2, x->stream));
+    if (s.sent) HIPCHK(hipMemsetAsync(s.sent, 0, 8ull << x->slog2, x->stream));
     HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
     s.n_cur = 0; s.cur_base = 0; s.cur_start = 0;
     s.viol_mask = 0; s.viol_in_model = 0; s.viol_inst = -1; s.viol_parent = 0; s.viol_child = ~0ull;
@@ -1131,10 +1196,14 @@ extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
 
 // ---- multi-shard exchange (transport: device copies for local shards, RCCL across ranks)
 //
-// One exchange round costs two host synchronisations: (1) after the expand
-// launches, to learn every (sender, owner) record count, which sizes the
-// fingerprint and answer transfers; (2) after the owners' inserts, to learn
-// every (owner, sender) winner count, which sizes the row transfers.
+// Two-phase: only fingerprints and answers cross shards.
+// One exchange round: the level kernel queues (fingerprint, parent) records
+// of successors other shards own; ONE host synchronisation learns every
+// (sender, owner) record count, which sizes the fingerprint transfer and the
+// answers coming back; the owners insert and answer new / seen; each sender
+// builds its winners into its own next level (k_build_winners).  At the
+// level's end the shards' next levels are re-balanced (rebalance) -- the only
+// rows that ever move, and only what drifted from an even split.
 
 // One exchange between the shards of this process: device copies, or (rccl_local)
 // one RCCL group of ncclSend/ncclRecv pairs to rank 0 -- this process -- issued
@@ -1219,21 +1288,13 @@ static int move_fps(rtla_ctx* x) {
   return comm_exchange(x, sends, recvs);
 }
 
-// (2) Owners answered in recv_ans (0 = seen, 1 + rank = new): route the
-// answers back into send_ans; h_new_out[p] = winners owner p has from this
-// shard, h_new_in[p] = rows this owner will receive from p.
+// (2) Owners answered in recv_ans (0 = seen, nonzero = new): route the
+// answers back into the senders' send_ans (sizes known since gather_counts:
+// no synchronisation).
 static int move_answers(rtla_ctx* x) {
   const int G = x->nshard;
   const uint64_t cap = x->box_cap;
   if (x->world == 1) {
-    for (auto& s : x->sh) {
-      if (x->rccl_local) {
-        if (int rc = comm_allgather(x, s.new_count, s.all_new, G)) return rc;
-        HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.all_new, 8 * G, hipMemcpyDeviceToHost, x->stream));
-      } else {
-        HIPCHK(hipMemcpyAsync(s.h_new_in.data(), s.new_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
-      }
-    }
     Local lc(x);
     for (auto& src : x->sh)
       for (auto& dst : x->sh) {
@@ -1242,11 +1303,7 @@ static int move_answers(rtla_ctx* x) {
           if (int rc = lc.move(src.send_ans + (uint64_t)dst.id * cap, dst.recv_ans + (uint64_t)src.id * cap, 4 * n))
             return rc;
       }
-    if (int rc = lc.flush()) return rc;
-    HIPCHK(hipStreamSynchronize(x->stream));
-    for (auto& src : x->sh)
-      for (auto& dst : x->sh) src.h_new_out[dst.id] = dst.h_new_in[src.id];
-    return RTLA_OK;
+    return lc.flush();
   }
   Shard& s = x->sh[0];
   std::vector<Msg> sends, recvs;
@@ -1255,58 +1312,110 @@ static int move_answers(rtla_ctx* x) {
     if (s.h_in[p]) sends.push_back({s.recv_ans + (uint64_t)p * cap, 4 * s.h_in[p], p});
     if (s.h_out[p]) recvs.push_back({s.send_ans + (uint64_t)p * cap, 4 * s.h_out[p], p});
   }
-  if (int rc = comm_exchange(x, sends, recvs)) return rc;
-  if (int rc = comm_allgather(x, s.new_count, s.all_new, G)) return rc;
-  HIPCHK(hipMemcpyAsync(s.h_all.data(), s.all_new, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
-  for (int p = 0; p < G; p++) {
-    s.h_new_in[p] = s.h_all[(size_t)s.id * G + p];   // owner s.id: new from source p
-    s.h_new_out[p] = s.h_all[(size_t)p * G + s.id];  // owner p: new from us
-  }
-  return RTLA_OK;
-}
-
-// Largest winner count of any (owner, sender) pair in the whole job: every
-// rank runs the same number of row sub-rounds.
-static uint64_t most_winners(rtla_ctx* x) {
-  uint64_t most = 0;
-  if (x->world == 1) {
-    for (auto& s : x->sh)
-      for (uint64_t v : s.h_new_in) most = std::max(most, v);
-  } else {
-    for (uint64_t v : x->sh[0].h_all) most = std::max(most, v);
-  }
-  return most;
-}
-
-// Ship the winners of ranks [lo, lo + rows_cap) to their owners; rows_in is
-// derived on the device from the owner's new_count (no host round trip).
-static int move_rows(rtla_ctx* x, uint64_t lo) {
-  const int G = x->nshard;
-  const uint64_t rc = x->rows_cap, RW = (uint64_t)x->L.W + 2;
-  auto part = [&](uint64_t n) { return n > lo ? std::min<uint64_t>(n - lo, rc) : 0; };
-  for (auto& s : x->sh) HIPCHK(launch_part_counts(s.new_count, G, lo, rc, s.rows_in, s.rows_base, s.ctr, x->stream));
-  if (x->world == 1) {
-    Local lc(x);
-    for (auto& dst : x->sh)
-      for (auto& src : x->sh) {
-        const uint64_t n = part(src.h_new_out[dst.id]);
-        if (n)
-          if (int r = lc.move(dst.recv_rows + (uint64_t)src.id * rc * RW, src.send_rows + (uint64_t)dst.id * rc * RW,
-                              4 * n * RW))
-            return r;
-      }
-    return lc.flush();
-  }
-  Shard& s = x->sh[0];
-  std::vector<Msg> sends, recvs;
-  for (int p = 0; p < G; p++) {
-    if (p == s.id) continue;
-    const uint64_t no = part(s.h_new_out[p]), ni = part(s.h_new_in[p]);
-    if (no) sends.push_back({s.send_rows + (uint64_t)p * rc * RW, 4 * no * RW, p});
-    if (ni) recvs.push_back({s.recv_rows + (uint64_t)p * rc * RW, 4 * ni * RW, p});
-  }
   return comm_exchange(x, sends, recvs);
+}
+
+// Level end: even out the shards' next levels.  n[k] = next-level states of
+// shard k (global ids, the same on every rank); the split every rank computes
+// alike is total / G each (the first total % G shards one more); shards
+// above it send their LAST rows, in shard order, to those below it (rows and
+// parent records, staged k_stage_rows -> exchange -> k_unpack_rows, in
+// sub-rounds of rows_cap).  Skipped while the largest excess is within
+// 2 % + 4096 rows of the split: a new state is stored by the shard that
+// generated it, so an even level stays about even, and after the first
+// levels (Init's successors all come from Init's shard) little moves.
+static int rebalance(rtla_ctx* x, std::vector<uint64_t>& n, const std::vector<uint64_t>& next_base,
+                     const std::vector<uint64_t>& next_cap) {
+  const int G = x->nshard;
+  uint64_t total = 0;
+  for (int k = 0; k < G; k++) total += n[k];
+  std::vector<uint64_t> tgt(G);
+  uint64_t worst = 0;
+  for (int k = 0; k < G; k++) {
+    tgt[k] = total / G + ((uint64_t)k < total % G ? 1 : 0);
+    if (n[k] > tgt[k]) worst = std::max(worst, n[k] - tgt[k]);
+  }
+  if (worst <= 4096 + total / (50ull * G)) return RTLA_OK;
+  auto local = [&](int id) -> Shard* {
+    for (auto& s : x->sh)
+      if (s.id == id) return &s;
+    return nullptr;
+  };
+  struct Move { int a, b; uint64_t first, base, cnt; };  // a's states [first, +cnt) -> b's slots [base, +cnt)
+  std::vector<Move> mv;
+  std::vector<uint64_t> m = n;
+  for (int a = 0, b = 0;;) {  // greedy, in shard order: the same plan on every rank
+    while (a < G && m[a] <= tgt[a]) a++;
+    while (b < G && m[b] >= tgt[b]) b++;
+    if (a >= G || b >= G) break;
+    const uint64_t c = std::min(m[a] - tgt[a], tgt[b] - m[b]);
+    mv.push_back({a, b, m[a] - c, m[b], c});
+    m[a] -= c;
+    m[b] += c;
+  }
+  // a receiver's room (its arena / parent records, as the level kernel's
+  // next_cap) is known only where it lives: if any lacks it, nobody moves
+  uint64_t short_of_room = 0;
+  for (size_t k = 0; k < x->sh.size(); k++)
+    if (m[x->sh[k].id] > next_cap[k]) short_of_room = 1;
+  if (x->world > 1)
+    if (int rc = allreduce_u64(x, &short_of_room, 1, 1)) return rc;
+  if (short_of_room || mv.empty()) return RTLA_OK;
+  const uint64_t rc = x->rows_cap, RW = (uint64_t)x->L.W + 2;
+  uint64_t most = 0;
+  for (auto& t : mv) most = std::max(most, t.cnt);
+  for (uint64_t lo = 0; lo < most; lo += rc) {
+    for (auto& s : x->sh) std::fill(s.h_reb, s.h_reb + 2 * SHARD_MAX, 0ull);
+    std::vector<Msg> sends, recvs;
+    Local lc(x);
+    uint64_t mx = 0;
+    for (auto& t : mv) {
+      if (t.cnt <= lo) continue;
+      const uint64_t c = std::min(rc, t.cnt - lo);
+      mx = std::max(mx, c);
+      Shard* sa = local(t.a);
+      Shard* sb = local(t.b);
+      if (sa) {
+        const size_t ka = (size_t)(sa - x->sh.data());
+        HIPCHK(launch_stage_rows(x->L.W, next_ring(x, *sa), sa->parents, next_base[ka], t.first + lo, c,
+                                 sa->send_rows + (uint64_t)t.b * rc * RW, x->stream));
+      }
+      if (sb) {
+        sb->h_reb[t.a] = c;
+        sb->h_reb[SHARD_MAX + t.a] = t.base + lo;
+      }
+      if (x->world == 1) {
+        if (int r = lc.move(sb->recv_rows + (uint64_t)t.a * rc * RW, sa->send_rows + (uint64_t)t.b * rc * RW,
+                            4 * c * RW))
+          return r;
+      } else if (sa) {
+        sends.push_back({sa->send_rows + (uint64_t)t.b * rc * RW, 4 * c * RW, t.b});
+      } else if (sb) {
+        recvs.push_back({sb->recv_rows + (uint64_t)t.a * rc * RW, 4 * c * RW, t.a});
+      }
+    }
+    if (x->world == 1) {
+      if (int r = lc.flush()) return r;
+    } else if (int r = comm_exchange(x, sends, recvs)) {
+      return r;
+    }
+    for (size_t k = 0; k < x->sh.size(); k++) {
+      Shard& s = x->sh[k];
+      bool any = false;
+      for (int p = 0; p < G; p++) any |= s.h_reb[p] != 0;
+      if (!any) continue;
+      HIPCHK(hipMemcpyAsync(s.rows_in, s.h_reb, 8 * G, hipMemcpyHostToDevice, x->stream));
+      HIPCHK(hipMemcpyAsync(s.rows_base, s.h_reb + SHARD_MAX, 8 * G, hipMemcpyHostToDevice, x->stream));
+      HIPCHK(launch_unpack_rows(x->L.W, s.recv_rows, s.rows_in, s.rows_base, G, rc, next_ring(x, s), s.parents,
+                                next_base[k], next_cap[k], s.ctr, mx, x->stream));
+    }
+    HIPCHK(hipStreamSynchronize(x->stream));  // (h_reb is rewritten by the next sub-round)
+  }
+  for (auto& t : mv) {
+    if (local(t.a)) x->rebalanced += t.cnt;
+  }
+  n = m;
+  return RTLA_OK;
 }
 
 // RTLA_STAMPS builds with RTLA_STAMPS_PRINT set: where the level kernel's
@@ -1344,7 +1453,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev0, x->stream));
   if (G == 1) {
     Shard& s = x->sh[0];
-    ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+    ShardBox box{1, 0, 0, 0, nullptr, nullptr, nullptr};
     uint64_t blocks = (s.n_cur + 3) / 4;
     int grid = (int)std::min<uint64_t>(blocks, (uint64_t)x->grid);
     HIPCHK(hipEventRecord(s.evm, x->stream));  // (re-recorded after the level kernel)
@@ -1359,7 +1468,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
         Shard& s = x->sh[k];
         uint64_t b = std::min<uint64_t>(c * x->chunk, s.n_cur), e = std::min<uint64_t>(b + x->chunk, s.n_cur);
         HIPCHK(hipMemsetAsync(s.out_count, 0, 8 * G, x->stream));
-        ShardBox box{G, s.id, (unsigned long long)x->box_cap, (unsigned long long*)s.out_count,
+        ShardBox box{G, s.id, (unsigned long long)x->box_cap, x->slog2, (unsigned long long*)s.out_count,
                      (unsigned long long*)s.send_fp, (unsigned long long*)s.send_ref};
         uint64_t blocks = (e - b + 3) / 4;
         int grid = (int)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), (uint64_t)x->grid);
@@ -1379,31 +1488,19 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
       }
       rc = move_answers(x);
       if (rc) return rc;
-      const uint64_t most = most_winners(x);
-      for (uint64_t lo = 0; lo < most; lo += x->rows_cap) {
-        for (size_t k = 0; k < x->sh.size(); k++) {
-          Shard& s = x->sh[k];
-          uint64_t mx_out = 0;
-          for (uint64_t v : s.h_out) mx_out = std::max(mx_out, v);
-          HIPCHK(launch_pack_rows(L, cur_ring(x, s), s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
-                                  x->box_cap, lo, lo + x->rows_cap, s.send_rows, x->rows_cap, s.ctr, mx_out,
-                                  x->stream));
-        }
-        rc = move_rows(x, lo);
-        if (rc) return rc;
-        for (size_t k = 0; k < x->sh.size(); k++) {
-          Shard& s = x->sh[k];
-          uint64_t mx_rows = 0;
-          for (uint64_t v : s.h_new_in) mx_rows = std::max(mx_rows, v > lo ? std::min(v - lo, x->rows_cap) : 0);
-          HIPCHK(launch_unpack_rows(L.W, s.recv_rows, s.rows_in, s.rows_base, G, x->rows_cap, next_ring(x, s),
-                                    s.parents, next_base[k], next_cap[k], s.ctr, mx_rows, x->stream));
-        }
+      for (size_t k = 0; k < x->sh.size(); k++) {  // each sender builds its winners into its own next level
+        Shard& s = x->sh[k];
+        uint64_t mx_out = 0;
+        for (uint64_t v : s.h_out) mx_out = std::max(mx_out, v);
+        HIPCHK(launch_build_winners(L, cur_ring(x, s), s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
+                                    x->box_cap, next_ring(x, s), s.parents, next_base[k], next_cap[k], s.ctr, mx_out,
+                                    x->stream));
       }
     }
   }
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev1, x->stream));
   // gather counters
-  uint64_t sums[4] = {0, 0, 0, 0};  // new, generated, probes, frontier
+  uint64_t sums[4 + SHARD_MAX] = {};  // new, generated, probes, frontier, next-level states per shard (global id)
   uint64_t maxs[4] = {0, 0, 0, 0};  // flags, violation, device time (us), largest next frontier of a shard
   double emax = 0.0;  // probe-kernel (k_expand_*) time of this level, ms
   std::vector<DevCounters> hc(x->sh.size());
@@ -1418,6 +1515,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     else ems = kms;  // multi-shard: rows are built inside the exchange rounds
     emax = std::max(emax, (double)ems);
     sums[0] += hc[k].next_count; sums[1] += hc[k].generated; sums[2] += hc[k].probes; sums[3] += s.n_cur;
+    sums[4 + s.id] = hc[k].next_count;
     maxs[0] |= (uint64_t)hc[k].flags;
     maxs[1] = std::max<uint64_t>(maxs[1], hc[k].viol_mask ? 1 : 0);
     maxs[2] = std::max<uint64_t>(maxs[2], (uint64_t)(kms * 1000.0));
@@ -1428,7 +1526,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     }
   }
   print_stamps(hc[0], x->level + 1);
-  int rc = allreduce2_u64(x, sums, 4, maxs, 4);
+  int rc = allreduce2_u64(x, sums, 4 + (G > 1 ? G : 0), maxs, 4);
   if (rc) return rc;
   x->max_front = maxs[3];
   if (maxs[0]) {
@@ -1454,11 +1552,16 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     x->finished = true;
     status = RTLA_DONE;
   }
+  std::vector<uint64_t> nnext(sums + 4, sums + 4 + G);
+  if (G > 1 && status == RTLA_OK) {  // even out the shards' next levels (rows stay with their senders)
+    if (int r = rebalance(x, nnext, next_base, next_cap)) return r;
+    x->max_front = *std::max_element(nnext.begin(), nnext.end());
+  }
   for (size_t k = 0; k < x->sh.size(); k++) {
     Shard& s = x->sh[k];
     s.cur_base = next_base[k];
     s.cur_start = next_ring(x, s).start;
-    s.n_cur = hc[k].next_count;
+    s.n_cur = G > 1 ? nnext[s.id] : hc[k].next_count;
   }
   if (st) {
     memset(st, 0, sizeof *st);
@@ -1505,18 +1608,24 @@ extern "C" int rtla_frontier(rtla_ctx* x, uint32_t* rows, size_t cap, size_t* n)
 
 // Digest of the current frontier: rows stream to the host in chunks (the
 // next chunk's copy overlaps the current chunk's hashing).
-extern "C" int rtla_level_text_hash(rtla_ctx* x, int threads, uint64_t* out) {
+static int level_digest(rtla_ctx* x, int threads, uint64_t* out, bool orbit) {
   if (!x || !out) return RTLA_E_ARG;
   if (!x->inited) return RTLA_E_STATE;
-  HIPCHK(hipSetDevice(x->device));
+  // A local failure (device, pinned buffers, a copy) skips the hashing but
+  // still reaches the reduction below, so no other rank waits in it.
+  int rc = hipSetDevice(x->device) == hipSuccess ? RTLA_OK : RTLA_E_HIP;
   const int W = x->L.W;
   const int nt = text_threads(threads);
   const uint64_t CH = std::max<uint64_t>(1, (256ull << 20) / (4ull * W));  // ~256 MB of rows per chunk
   uint32_t* hbuf[2] = {nullptr, nullptr};
-  for (auto& b : hbuf) HIPCHK(hipHostMalloc((void**)&b, CH * W * 4, hipHostMallocDefault));
+  for (auto& b : hbuf)
+    if (!rc && hipHostMalloc((void**)&b, CH * W * 4, hipHostMallocDefault) != hipSuccess) {
+      b = nullptr;
+      rc = RTLA_E_HIP;
+    }
   uint64_t sum = 0;
-  int rc = RTLA_OK;
   for (auto& s : x->sh) {
+    if (rc) break;
     const Ring r = cur_ring(x, s);
     // chunk j covers states [j * CH, ...); copies go in pieces that do not wrap the ring
     auto issue = [&](uint64_t g0, uint32_t* dst) -> hipError_t {
@@ -1536,12 +1645,13 @@ extern "C" int rtla_level_text_hash(rtla_ctx* x, int threads, uint64_t* out) {
     for (uint64_t g = 0, j = 0; g < s.n_cur; g += CH, j++) {
       if (hipStreamSynchronize(x->stream) != hipSuccess) { rc = RTLA_E_HIP; break; }
       if (g + CH < s.n_cur && issue(g + CH, hbuf[(j + 1) & 1]) != hipSuccess) { rc = RTLA_E_HIP; break; }
-      sum += rows_digest(x->L, hbuf[j & 1], std::min<uint64_t>(CH, s.n_cur - g), nt);
+      sum += rows_digest(x->L, hbuf[j & 1], std::min<uint64_t>(CH, s.n_cur - g), nt, orbit);
     }
     if (rc) break;
   }
   (void)hipStreamSynchronize(x->stream);
-  for (auto& b : hbuf) (void)hipHostFree(b);
+  for (auto& b : hbuf)
+    if (b) (void)hipHostFree(b);
   // every rank joins the reduction, also after a local failure (the flag travels with it)
   uint64_t v[2] = {sum, rc ? 1ull : 0ull};
   if (int e = allreduce_u64(x, v, 2, 0)) return e;
@@ -1549,6 +1659,13 @@ extern "C" int rtla_level_text_hash(rtla_ctx* x, int threads, uint64_t* out) {
   if (v[1]) return RTLA_E_HIP;
   *out = v[0];
   return RTLA_OK;
+}
+
+extern "C" int rtla_level_text_hash(rtla_ctx* x, int threads, uint64_t* out) {
+  return level_digest(x, threads, out, false);
+}
+extern "C" int rtla_level_orbit_hash(rtla_ctx* x, int threads, uint64_t* out) {
+  return level_digest(x, threads, out, true);
 }
 
 extern "C" int rtla_coverage(rtla_ctx* x, uint64_t* gen, uint64_t* distinct, int n) {
@@ -1687,7 +1804,7 @@ extern "C" int rtla_synthetic_dedup(rtla_ctx* x, uint64_t begin, uint64_t end, r
   s.h_caps[0] = end; s.h_caps[1] = 0; s.h_caps[2] = s.parents_cap;
   HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
   const Ring ring{s.arena, 0, x->front_cap};
-  ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+  ShardBox box{1, 0, 0, 0, nullptr, nullptr, nullptr};
   HIPCHK(hipEventRecord(s.ev0, x->stream));
   HIPCHK(launch_expand(x->L, ring, begin, end, 0, ring, s.parents, 0, 0, s.table, x->tlog2, s.ctr, box, x->grid,
                        x->stream, env_xflags() | XF_DEDUP_ONLY));
@@ -1729,7 +1846,7 @@ extern "C" int rtla_time_expand(rtla_ctx* x, int xflags, int reps, double* ms) {
   const uint64_t next_base = s.cur_base + s.n_cur;
   if (next_base >= s.parents_cap) return RTLA_E_OVERFLOW;
   const uint64_t next_cap = std::min<uint64_t>(next_room(x, s), s.parents_cap - next_base);
-  ShardBox box{1, 0, 0, nullptr, nullptr, nullptr};
+  ShardBox box{1, 0, 0, 0, nullptr, nullptr, nullptr};
   float total = 0.f;
   for (int r = 0; r < reps; r++) {
     HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
@@ -1780,6 +1897,44 @@ extern "C" int rtla_probe_bench2(int log2, uint64_t n, double* s_insert, double*
   (void)hipFree(table);
   (void)hipFree(ctr);
   return RTLA_OK;
+}
+
+extern "C" int rtla_probe_bench3(int log2, uint64_t n_present, uint64_t n, double new_frac, double* seconds,
+                                 uint64_t* inserted) {
+  if (log2 < 16 || log2 > 36 || !n || n_present >= (1ull << log2)) return RTLA_E_ARG;
+  uint64_t* table = nullptr;
+  DevCounters* ctr = nullptr;
+  HIPCHK(hipMalloc(&table, 8ull << log2));
+  int rc = RTLA_OK;
+  if (hipMalloc(&ctr, sizeof(DevCounters)) != hipSuccess) rc = RTLA_E_HIP;
+  hipEvent_t e[2] = {nullptr, nullptr};
+  float ms = 0.f;
+  DevCounters h;
+  memset(&h, 0, sizeof h);
+  auto step = [&](hipError_t v) {
+    if (!rc && v != hipSuccess) rc = RTLA_E_HIP;
+  };
+  step(hipMemset(table, 0, 8ull << log2));
+  if (!rc) step(hipMemset(ctr, 0, sizeof(DevCounters)));
+  for (auto& v : e)
+    if (!rc) step(hipEventCreate(&v));
+  if (!rc) step(launch_probe_bench(table, log2, n_present, 777, ctr, nullptr, 0));  // the present keys (untimed)
+  if (!rc) step(hipMemset(ctr, 0, sizeof(DevCounters)));
+  if (!rc) step(hipDeviceSynchronize());
+  if (!rc) step(hipEventRecord(e[0], nullptr));
+  if (!rc) step(launch_probe_mixed(table, log2, n, n_present, new_frac, 777, ctr, nullptr));
+  if (!rc) step(hipEventRecord(e[1], nullptr));
+  if (!rc) step(hipEventSynchronize(e[1]));
+  if (!rc) step(hipEventElapsedTime(&ms, e[0], e[1]));
+  if (!rc) step(hipMemcpy(&h, ctr, sizeof h, hipMemcpyDeviceToHost));
+  if (!rc && (h.flags & FLAG_FPSET_FULL)) rc = RTLA_E_OVERFLOW;
+  if (seconds) *seconds = ms / 1e3;
+  if (inserted) *inserted = h.next_count;
+  for (auto& v : e)
+    if (v) (void)hipEventDestroy(v);
+  (void)hipFree(table);
+  if (ctr) (void)hipFree(ctr);
+  return rc;
 }
 
 extern "C" int rtla_probe_bench(int log2, uint64_t n, double* seconds, uint64_t* inserted) {

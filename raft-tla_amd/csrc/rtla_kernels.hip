@@ -5,8 +5,8 @@
 // (rtla_kernels_common.h), picked here by layout from
 // the instantiation units (rtla_kspec_*, rtla_ksym_*, rtla_kgeneric_*), or of
 // the wave-per-state fallback k_expand (rtla_kwave.hip).  This unit also
-// holds the multi-shard exchange kernels (k_insert_remote, k_unpack_rows,
-// k_part_counts), Init's insert, the synthetic microbench's state generator
+// holds the multi-shard exchange kernels (k_insert_remote, and the level-end
+// re-balancing's k_stage_rows / k_unpack_rows), Init's insert, the synthetic microbench's state generator
 // and the fingerprint-set calibration kernel.
 #include "rtla_kernels_common.h"
 
@@ -55,14 +55,13 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
   if (lane == 0 && probes) atomicAdd(&ctr->probes, (unsigned long long)probes);
 }
 
-// Owner side: append the received rows to the next frontier (one wave per
-// row, coalesced copy) with their cross-shard parent records.
+// Re-balancing, receiving side: append the staged rows to the next frontier
+// (one wave per row, coalesced copy) with their parent records.
 __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ counts,
                               const unsigned long long* __restrict__ bases, int nshard, unsigned long long rows_cap,
                               Ring next, unsigned long long* __restrict__ parents,
                               unsigned long long next_base, unsigned long long next_cap, DevCounters* ctr) {
   // grid.y = source shard p; its rows land at the contiguous slots bases[p] + k
-  // (bases from k_part_counts: no per-row atomics)
   const unsigned long long p = blockIdx.y;
   const unsigned long long n = counts[p], base = bases[p];
   const int lane = threadIdx.x & 63;
@@ -82,21 +81,26 @@ __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const un
   }
 }
 
-// rows_in[p] = the part [lo, lo + rc) of the new_count[p] rows owner-side.
-// and bases[p] = the next-frontier slot of its first row; advances next_count.
-__global__ void k_part_counts(const unsigned long long* __restrict__ new_count, int nshard, unsigned long long lo,
-                              unsigned long long rc, unsigned long long* __restrict__ rows_in,
-                              unsigned long long* __restrict__ bases, DevCounters* ctr) {
-  if (threadIdx.x != 0) return;
-  unsigned long long b = ctr->next_count;
-  for (int p = 0; p < nshard; p++) {
-    const unsigned long long n = new_count[p];
-    const unsigned long long r = n > lo ? min(n - lo, rc) : 0ull;
-    rows_in[p] = r;
-    bases[p] = b;
-    b += r;
+// Re-balancing (rtla_step, level end): copy states [first, first + n) of a
+// shard's next level -- rows and parent records -- into a staging region of
+// n slots of W + 2 words (the k_unpack_rows format), one wave per row.
+__global__ void k_stage_rows(int W, Ring next, const unsigned long long* __restrict__ parents,
+                             unsigned long long next_base, unsigned long long first, unsigned long long n,
+                             uint32_t* __restrict__ rows) {
+  const int lane = threadIdx.x & 63;
+  const int RW = W + 2;
+  const unsigned long long wv = (blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x) >> 6;
+  const unsigned long long nw = ((unsigned long long)gridDim.x * blockDim.x) >> 6;
+  for (unsigned long long k = wv; k < n; k += nw) {
+    const uint32_t* src = ring_row(next, first + k, W);
+    uint32_t* dst = rows + k * (unsigned long long)RW;
+    for (int w = lane; w < W; w += 64) dst[w] = src[w];
+    if (lane == 0) {
+      const unsigned long long pr = parents[next_base + first + k];
+      dst[W] = (uint32_t)pr;
+      dst[W + 1] = (uint32_t)(pr >> 32);
+    }
   }
-  ctr->next_count = b;
 }
 
 // Insert the fingerprints of `n` rows (Init).  new_flags[i] = 1 if new.
@@ -145,6 +149,27 @@ __global__ void k_probe_bench(unsigned long long* table, int tlog2, unsigned lon
     } else {
       got += fpset_insert(table, tlog2, f) == 1;
     }
+  }
+  for (int off = 32; off > 0; off >>= 1) got += __shfl_down(got, off);
+  if ((threadIdx.x & 63) == 0 && got) atomicAdd(&ctr->next_count, got);
+}
+
+// Mixed-stream calibration (bench.py's random-access ceiling): probe i is,
+// with probability new_frac (threshold q of 2^64), a key never inserted
+// before, else one of the n_present keys inserted beforehand -- the level
+// kernel's protocol on each: load the home slot, CAS only when it reads
+// empty (linear probing on).  ctr->next_count counts the inserts.
+__global__ void k_probe_mixed(unsigned long long* table, int tlog2, unsigned long long n, unsigned long long n_present,
+                              unsigned long long q, unsigned long long seed, DevCounters* ctr) {
+  unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  unsigned long long got = 0;
+  for (; i < n; i += stride) {
+    const FP pick = hash_u64(seed ^ 0x6d69786564ull, i);
+    const FP f = pick.a < q ? hash_u64(seed + 1, i) : hash_u64(seed, pick.b % n_present);
+    const unsigned long long idx = f.a >> (64 - tlog2);
+    const unsigned long long v = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    got += fpset_resolve_loaded(table, tlog2, f.b | 1ull, idx, v, ctr) ? 1 : 0;
   }
   for (int off = 32; off > 0; off >>= 1) got += __shfl_down(got, off);
   if ((threadIdx.x & 63) == 0 && got) atomicAdd(&ctr->next_count, got);
@@ -236,11 +261,12 @@ hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* count
   return hipGetLastError();
 }
 
-hipError_t launch_part_counts(const uint64_t* new_count, int nshard, uint64_t lo, uint64_t rc, uint64_t* rows_in,
-                              uint64_t* bases, DevCounters* ctr, hipStream_t st) {
-  hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, (const unsigned long long*)new_count, nshard,
-                     (unsigned long long)lo, (unsigned long long)rc, (unsigned long long*)rows_in,
-                     (unsigned long long*)bases, ctr);
+hipError_t launch_stage_rows(int W, const Ring& next, const uint64_t* parents, uint64_t next_base, uint64_t first,
+                             uint64_t n, uint32_t* rows, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_stage_rows, dim3(grid_x(n, 4)), dim3(256), 0, st, W, next,
+                     (const unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)first,
+                     (unsigned long long)n, rows);
   return hipGetLastError();
 }
 
@@ -266,6 +292,16 @@ hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t s
                               hipStream_t st, int load_first) {
   hipLaunchKernelGGL(k_probe_bench, dim3(256 * 16), dim3(256), 0, st, (unsigned long long*)table, tlog2,
                      (unsigned long long)n, (unsigned long long)seed, ctr, load_first);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_mixed(uint64_t* table, int tlog2, uint64_t n, uint64_t n_present, double new_frac,
+                              uint64_t seed, DevCounters* ctr, hipStream_t st) {
+  const double qf = std::min(1.0, std::max(0.0, new_frac)) * 18446744073709551616.0;
+  const unsigned long long q = qf >= 18446744073709551615.0 ? ~0ull : (unsigned long long)qf;
+  hipLaunchKernelGGL(k_probe_mixed, dim3(256 * 16), dim3(256), 0, st, (unsigned long long*)table, tlog2,
+                     (unsigned long long)n, (unsigned long long)std::max<uint64_t>(n_present, 1), q,
+                     (unsigned long long)seed, ctr);
   return hipGetLastError();
 }
 

@@ -143,12 +143,9 @@ __device__ __forceinline__ bool claim_violation(DevCounters* c, int bad, int lan
 // Slots only ever change 0 -> key, so a slot holding the key proves the
 // state is present, and one holding another key can be skipped for good;
 // only an empty slot needs the CAS (which may then find the key after all).
-// lossy (the MULTI sent cache, a dedup hint only): a long probe chain answers
-// "not sent yet" -- the record is shipped and its owner deduplicates -- and
-// never raises FLAG_FPSET_FULL.
 __device__ __forceinline__ bool fpset_resolve_loaded(unsigned long long* table, int log2, unsigned long long key,
                                                      unsigned long long idx, unsigned long long seen,
-                                                     DevCounters* ctr, bool lossy = false) {
+                                                     DevCounters* ctr) {
   const unsigned long long mask = (1ull << log2) - 1ull;
   for (int probe = 1;; probe++) {
     if (seen == key) return false;
@@ -157,7 +154,6 @@ __device__ __forceinline__ bool fpset_resolve_loaded(unsigned long long* table, 
       if (seen == 0ull) return true;
       if (seen == key) return false;
     }
-    if (lossy && probe >= 64) return true;
     if (probe >= 4096) {
       set_flag(ctr, FLAG_FPSET_FULL);
       return false;
@@ -430,7 +426,7 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 }  // namespace
 
 #ifndef RTLA_COMPACT_WAVES_PER_EU
-#define RTLA_COMPACT_WAVES_PER_EU 3  // 166 VGPRs for N = 3 without spills (the default allocation took 170 -> 2 waves)
+#define RTLA_COMPACT_WAVES_PER_EU 3  // 168 VGPRs (3 waves/SIMD); spills per instantiation: profiles/r04_*/resource_usage.txt
 #endif
 #ifndef RTLA_SYM_WAVES_PER_EU
 #define RTLA_SYM_WAVES_PER_EU 3      // SYMMETRY: 168 VGPRs with spills beats 256 without (configs[3]: 356 vs 406 ms)
@@ -526,9 +522,14 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
   RTLA_STAMP_DECL
   // pending probe (issued by the previous chunk).  MULTI: a successor owned
-  // by another shard probes this shard's SENT cache instead of the set: the
-  // first time this shard meets it, its (fingerprint, parent) record goes to
-  // the owner's outbox; later copies are dropped (the owner already has it).
+  // by another shard probes this shard's SENT cache instead of the set --
+  // a dedup hint, one slot per fingerprint (2^box.slog2 slots), overwritten
+  // on a miss: a hit drops the copy (this shard sent it to its owner
+  // already), a miss queues its (fingerprint, parent) record for the owner
+  // and stores the key in the slot (a plain store, issued like the CAS of a
+  // set insert and reported a chunk later).  Bounded work per probe, never
+  // full; a slot overwritten by another key only costs a duplicate record,
+  // which the owner deduplicates.
   bool pend = false;
   unsigned long long pold = 0;
   FP pf{0, 0};       // its fingerprint (home slot and owner derive from it)
@@ -537,8 +538,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // the home slot if it read empty, else at the next slot (linear probing;
   // slots only ever go 0 -> key) -- together with the next chunk's loads,
   // and that CAS is resolved a chunk later: neither the insert nor the first
-  // collision step waits for a round trip.  (MULTI: in the set or, for a
-  // successor another shard owns, in the sent cache.)
+  // collision step waits for a round trip.  (MULTI, a successor another
+  // shard owns: the sent-cache store instead, see above.)
   const bool async_cas = (!MULTI || RTLA_MULTI_ASYNC) && !(xflags & XF_CAS_ONLY);
   bool cpend = false;    // CAS set up by resolve(), issued by issue_cas()
   bool cflight = false;  // CAS in flight (result in cold)
@@ -690,7 +691,14 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 #ifdef RTLA_COUNT_CAS
     if (cpend) my_cas++;
 #endif
-    if (cpend) cold = atomicCAS(&((MULTI && cowner != me) ? sent : table)[cidx], 0ull, ckey);
+    if (cpend) {
+      if (MULTI && cowner != me) {  // the sent cache: overwrite, report "not sent before"
+        sent[cidx] = ckey;
+        cold = 0ull;
+      } else {
+        cold = atomicCAS(&table[cidx], 0ull, ckey);
+      }
+    }
     cflight = cpend;
     cpend = false;
   };
@@ -706,17 +714,19 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     } else if (async_cas) {
       if (cflight) {  // the CAS issued one chunk ago
         if (cold == 0ull) isnew = true;
-        else if (cold != ckey)  // rare: keep probing
-          isnew = fpset_resolve((MULTI && cowner != me) ? sent : table, tlog2, ckey, cidx, cold, ctr);
+        else if (cold != ckey)  // rare: keep probing (the set only: a sent-cache store reports 0)
+          isnew = fpset_resolve(table, tlog2, ckey, cidx, cold, ctr);
       }
       ninfo = cinfo;
       nf = cf;
       nowner_r = cowner;
       cflight = false;
-      if (pend) {  // this chunk's load -> seen, or a CAS for the next issue
-        const unsigned long long key = pf.b | 1ull, idx = pf.a >> (64 - tlog2);
+      if (pend) {  // this chunk's load -> seen, or a CAS (sent cache: a store) for the next issue
+        const bool to_sent = MULTI && powner != me;
+        const int lg = to_sent ? box.slog2 : tlog2;
+        const unsigned long long key = pf.b | 1ull, idx = pf.a >> (64 - lg);
         if (pold != key) {
-          cidx = pold == 0ull ? idx : ((idx + 1ull) & ((1ull << tlog2) - 1ull));
+          cidx = (to_sent || pold == 0ull) ? idx : ((idx + 1ull) & ((1ull << lg) - 1ull));
           ckey = key;
           cinfo = pinfo;
           if (MULTI) {
@@ -727,11 +737,14 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         }
       }
     } else if (pend) {
-      const bool to_sent = MULTI && powner != me;
-      unsigned long long* t = to_sent ? sent : table;
-      const unsigned long long pidx = pf.a >> (64 - tlog2);
-      isnew = (xflags & XF_CAS_ONLY) ? fpset_resolve(t, tlog2, pf.b | 1ull, pidx, pold, ctr)
-                                     : fpset_resolve_loaded(t, tlog2, pf.b | 1ull, pidx, pold, ctr, to_sent);
+      if (MULTI && powner != me) {  // the sent cache: a miss overwrites the slot
+        isnew = pold != (pf.b | 1ull);
+        if (isnew) sent[pf.a >> (64 - box.slog2)] = pf.b | 1ull;
+      } else {
+        const unsigned long long pidx = pf.a >> (64 - tlog2);
+        isnew = (xflags & XF_CAS_ONLY) ? fpset_resolve(table, tlog2, pf.b | 1ull, pidx, pold, ctr)
+                                       : fpset_resolve_loaded(table, tlog2, pf.b | 1ull, pidx, pold, ctr);
+      }
     }
     if (MULTI) {  // records for other owners: one outbox reservation per (wave, owner)
       const int powner = nowner_r;
@@ -853,8 +866,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           if constexpr (SYM) key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
           nprobe = !(xflags & XF_NO_PROBE);
           ncf = key;
-          nidx = key.a >> (64 - tlog2);
           nowner = MULTI ? fp_owner(key, box.nshard) : me;
+          nidx = key.a >> (64 - ((MULTI && nowner != me) ? box.slog2 : tlog2));
         }
       }
     }
@@ -909,8 +922,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       const FP key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
       nprobe = !(xflags & XF_NO_PROBE);
       ncf = key;
-      nidx = key.a >> (64 - tlog2);
       nowner = MULTI ? fp_owner(key, box.nshard) : me;
+      nidx = key.a >> (64 - ((MULTI && nowner != me) ? box.slog2 : tlog2));
     }
   };
   auto issue_probe = [&]() {
@@ -926,8 +939,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       // load is cheaper than an atomic at the memory side; the CAS is
       // only issued (at resolve time) when the home slot reads empty
       if (!(xflags & XF_ALL_SUCCESSORS))
-        pold = (xflags & XF_CAS_ONLY) ? atomicCAS(slotp, 0ull, ncf.b | 1ull)
-                                      : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pold = ((xflags & XF_CAS_ONLY) && !(MULTI && nowner != me))
+                   ? atomicCAS(slotp, 0ull, ncf.b | 1ull)
+                   : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     nprobe = false;
   };

@@ -1,48 +1,50 @@
 // rtla_kpack.hip -- lane-per-state row builders: the multi-shard sender's
-// k_pack_rows and the wave-per-state k_expand_batch (the parity seam's
+// k_build_winners and the wave-per-state k_expand_batch (the parity seam's
 // fallback for rows too wide for the level kernel).
 #include "rtla_kernels_common.h"
 
-// Sender side: materialise the queued successors whose owner answered "new"
-// with a rank in [lo, hi) into the owner's row region (row + parent record,
-// RW = W + 2 words per slot).  Invariants are checked here, where parent and
-// action are known; a violation is recorded against the local parent.
-template <int NS>
+// Sender side of the two-phase exchange: the owners
+// answered every queued (fingerprint, parent) record with "new" (nonzero) or
+// "seen"; the sender builds each winner ITSELF -- gathers its parent row
+// (this shard's current level) into LDS, recomputes the successor's Delta,
+// patches the row in place -- and appends it to ITS OWN next level with a
+// local parent record.  No row crosses shards (the owner keeps only the
+// fingerprint), so the next levels of the shards stay as balanced as their
+// frontiers are (rtla_step re-balances what drifts).  Invariants and
+// distinct coverage are evaluated here, where parent and action are known.
+// LC: compiled-in layout (Layout{} = run-time Lrt), as for the level kernel.
+template <int NS, Layout LC>
 __global__ void __launch_bounds__(256)
-k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
-            const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
-            const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap, unsigned long long lo,
-            unsigned long long hi, uint32_t* __restrict__ rows, unsigned long long rows_cap, DevCounters* ctr) {
-  // A wave scans 64 records of owner p (grid.y), compacts the winners of
-  // this sub-round, gathers their parent rows into LDS (one coalesced read
-  // per row), builds each successor in place and ships row + parent record
-  // to the slot the owner's answer names (one coalesced write per row).
+k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
+                const unsigned long long* __restrict__ send_ref, const uint32_t* __restrict__ ans,
+                const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap, Ring next,
+                unsigned long long* __restrict__ parents, unsigned long long next_base, unsigned long long next_cap,
+                DevCounters* ctr) {
+  // A wave scans 64 records of owner p (grid.y), compacts the winners,
+  // gathers their parent rows into LDS (one coalesced read per row), builds
+  // each successor in place, reserves next-level slots with one atomic and
+  // stores the rows (one coalesced write per row) and parent records.
+  const Layout& L = pick_layout<LC>(Lrt);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
-  const int W = L.W, AW = L.all_words, RW = W + 2;
+  const int W = L.W, AW = L.all_words;
   uint32_t* lrows = lds + wave * lane_lds_words(W, AW);
   const LaneWords pall{lrows + 64 * W + lane};
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
   const unsigned long long p = blockIdx.y;  // owner shard
   const unsigned long long n = counts[p];
-  const unsigned long long below = (1ull << lane) - 1ull;
   for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; k0 < n;
        k0 += (unsigned long long)gridDim.x * wpb * 64ull) {
     const unsigned long long k = k0 + lane;
     const unsigned long long i = p * cap + k;
-    const unsigned long long a = k < n ? ans[i] : 0ull;
-    const bool win = a != 0 && a - 1 >= lo && a - 1 < hi;
+    const bool win = k < n && ans[i] != 0u;
     const unsigned long long m = __ballot(win);
     if (!m) continue;
     const int nw = __popcll(m);
-    // compact: winner number r of this wave = lane w_r
-    int r_of_lane = __popcll(m & below);
-    unsigned long long ref = win ? send_ref[i] : 0ull;
-    unsigned long long dslot = win ? a - 1 - lo : 0ull;
-    // lane r takes the r-th winner's (ref, dslot)
+    // lane r takes the r-th winner's record
     int src_lane = 0;
     {
       unsigned long long mm = m;
@@ -52,15 +54,16 @@ k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
         if (lane == r) src_lane = l;
       }
     }
-    (void)r_of_lane;
-    ref = shfl_u64(ref, src_lane);
-    dslot = shfl_u64(dslot, src_lane);
+    const unsigned long long ref = shfl_u64(win ? send_ref[i] : 0ull, src_lane);
     const bool act = lane < nw;
-    const unsigned long long s = ref >> 16;
+    const unsigned long long s = ref >> 16;  // parent: state s of the current level
     const int inst = (int)(ref & 0xffffull);
     gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
     wave_sync();
     uint32_t* prow = lrows + lane * W;
+    unsigned long long obase = 0;
+    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)nw);
+    obase = shfl0_u64(obase);
     if (act) {
       const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
       DeltaT<NS> d;
@@ -68,27 +71,21 @@ k_pack_rows(Layout L, Ring cur, unsigned long long cur_base, int me,
       const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
       const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
       if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-            atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+          atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
         ctr->viol_parent = cur_base + s;
         ctr->viol_inst = inst;
         ctr->viol_in_model = 1;
-        ctr->viol_child = ~0ull;
+        ctr->viol_child = obase + lane < next_cap ? next_base + obase + lane : ~0ull;
       }
       atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
       materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
     }
     wave_sync();
-    for (int r = 0; r < nw; r++) {
-      const unsigned long long ds = readlane_u64(dslot, r);
-      uint32_t* dst = rows + (p * rows_cap + ds) * (unsigned long long)RW;
-      for (int w = lane; w < W; w += 64) dst[w] = lrows[r * W + w];
-      if (lane == 0) {
-        const unsigned long long pr =
-            (unsigned long long)me << 56 | (cur_base + readlane_u64(s, r)) << 16 | (unsigned long long)__builtin_amdgcn_readlane(inst, r);
-        dst[W] = (uint32_t)pr;
-        dst[W + 1] = (uint32_t)(pr >> 32);
-      }
-    }
+    if (obase + nw > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nw, next_cap - obase);
+    store_rows_ring(next, obase, nrows, W, lrows, lane);
+    if (lane < nrows)
+      parents[next_base + obase + lane] = (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
     wave_sync();
   }
   __syncthreads();
@@ -159,18 +156,47 @@ k_expand_batch(Layout L, const uint32_t* __restrict__ rows, unsigned long long n
 
 namespace rtla {
 
-hipError_t launch_pack_rows(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
-                            const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
-                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, uint64_t max_count,
-                            hipStream_t st) {
-  if (!max_count) return hipSuccess;
+template <int NS, Layout LC>
+static hipError_t build_winners(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+                                const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, const Ring& next,
+                                uint64_t* parents, uint64_t next_base, uint64_t next_cap, DevCounters* ctr,
+                                uint64_t max_count, hipStream_t st) {
   const int wpb = std::max(1, expand_lane_wpb(L));
   const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-  RTLA_DISPATCH_N(L, k_pack_rows, dim3(grid_x(max_count, 64 * wpb), nshard), dim3(64 * wpb), lds, st, L, cur,
-                  (unsigned long long)cur_base, me, (const unsigned long long*)send_ref, ans,
-                  (const unsigned long long*)counts, nshard, (unsigned long long)cap, (unsigned long long)lo,
-                  (unsigned long long)hi, rows, (unsigned long long)rows_cap, ctr);
+  hipLaunchKernelGGL((k_build_winners<NS, LC>), dim3(grid_x(max_count, 64 * wpb), nshard), dim3(64 * wpb), lds, st,
+                     L, cur, (unsigned long long)cur_base, me, (const unsigned long long*)send_ref, ans,
+                     (const unsigned long long*)counts, nshard, (unsigned long long)cap, next,
+                     (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap, ctr);
   return hipGetLastError();
+}
+
+hipError_t launch_build_winners(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+                                const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap,
+                                const Ring& next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                                DevCounters* ctr, uint64_t max_count, hipStream_t st) {
+  if (!max_count) return hipSuccess;
+#define RTLA_BW(LC) \
+  return build_winners<LC.N, LC>(L, cur, cur_base, me, send_ref, ans, counts, nshard, cap, next, parents, next_base, \
+                                 next_cap, ctr, max_count, st)
+  // the BASELINE layouts bench.py shards (compiled in, as for the level kernel)
+  if (same_layout(L, specs::CFG2)) RTLA_BW(specs::CFG2);
+  if (same_layout(L, specs::CFG1)) RTLA_BW(specs::CFG1);
+  if (same_layout(L, specs::EXHAUST)) RTLA_BW(specs::EXHAUST);
+  if (same_layout(L, specs::CFG3)) RTLA_BW(specs::CFG3);
+  if (same_layout(L, specs::CFG4)) RTLA_BW(specs::CFG4);
+#undef RTLA_BW
+  switch (L.N) {
+    case 1: return build_winners<1, Layout{}>(L, cur, cur_base, me, send_ref, ans, counts, nshard, cap, next, parents,
+                                              next_base, next_cap, ctr, max_count, st);
+    case 2: return build_winners<2, Layout{}>(L, cur, cur_base, me, send_ref, ans, counts, nshard, cap, next, parents,
+                                              next_base, next_cap, ctr, max_count, st);
+    case 3: return build_winners<3, Layout{}>(L, cur, cur_base, me, send_ref, ans, counts, nshard, cap, next, parents,
+                                              next_base, next_cap, ctr, max_count, st);
+    case 4: return build_winners<4, Layout{}>(L, cur, cur_base, me, send_ref, ans, counts, nshard, cap, next, parents,
+                                              next_base, next_cap, ctr, max_count, st);
+    default: return build_winners<5, Layout{}>(L, cur, cur_base, me, send_ref, ans, counts, nshard, cap, next, parents,
+                                               next_base, next_cap, ctr, max_count, st);
+  }
 }
 
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out, uint64_t* info,

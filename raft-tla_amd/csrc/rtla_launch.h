@@ -9,7 +9,7 @@ namespace rtla {
 
 // LDS bytes a k_expand / k_expand_batch block of `wpb` waves needs.
 size_t expand_lds_bytes(const Layout& L, int wpb);
-// Waves per block of the lane-per-state row builders (k_pack_rows).
+// Waves per block of the lane-per-state row builders (k_build_winners).
 int expand_lane_wpb(const Layout& L);
 // Waves per block of the compacting level kernel (0: not usable).
 int expand_compact_wpb(const Layout& L);
@@ -56,15 +56,15 @@ hipError_t launch_wave_expand(const Layout& L, const Ring& cur, uint64_t s_begin
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
                                 uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
                                 uint64_t max_count, hipStream_t st);
-hipError_t launch_pack_rows(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
-                            const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, uint64_t lo,
-                            uint64_t hi, uint32_t* rows, uint64_t rows_cap, DevCounters* ctr, uint64_t max_count,
-                            hipStream_t st);
+hipError_t launch_build_winners(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
+                                const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap,
+                                const Ring& next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,
+                                DevCounters* ctr, uint64_t max_count, hipStream_t st);
 hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* counts, const uint64_t* bases, int nshard,
                               uint64_t rows_cap, const Ring& next, uint64_t* parents, uint64_t next_base,
                               uint64_t next_cap, DevCounters* ctr, uint64_t max_count, hipStream_t st);
-hipError_t launch_part_counts(const uint64_t* new_count, int nshard, uint64_t lo, uint64_t rc, uint64_t* rows_in,
-                              uint64_t* bases, DevCounters* ctr, hipStream_t st);
+hipError_t launch_stage_rows(int W, const Ring& next, const uint64_t* parents, uint64_t next_base, uint64_t first,
+                             uint64_t n, uint32_t* rows, hipStream_t st);
 hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
                               int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st);
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,
@@ -73,5 +73,7 @@ hipError_t launch_random_rows(const Layout& L, uint64_t seed, uint64_t first, ui
                               hipStream_t st);
 hipError_t launch_probe_bench(uint64_t* table, int tlog2, uint64_t n, uint64_t seed,
                               DevCounters* ctr, hipStream_t st, int load_first = 0);
+hipError_t launch_probe_mixed(uint64_t* table, int tlog2, uint64_t n, uint64_t n_present, double new_frac,
+                              uint64_t seed, DevCounters* ctr, hipStream_t st);
 
 }  // namespace rtla

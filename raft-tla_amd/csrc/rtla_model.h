@@ -98,7 +98,7 @@ enum {
   R_UPDATETERM = 0, R_HRVREQ, R_HRVRESP, R_HAEREQ, R_HAERESP, R_DROPSTALE, R_NONE
 };
 
-// Invariant bits (build-defined model wrapper, oracle/MC.tla).
+// Invariant bits (build-defined model wrapper, specs/MC.tla).
 enum { INV_NO_TWO_LEADERS = 1, INV_ELECTION_SAFETY = 2, INV_LOG_MATCHING = 4 };
 
 // A model's row format.  Plain ints only (a C++20 structural type): the

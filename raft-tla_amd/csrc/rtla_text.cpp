@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 
 namespace rtla {
 
@@ -90,7 +91,7 @@ void text_vl(Out& o, uint32_t dom, const uint32_t* vl, int N) {
 
 const char* BOOL(uint32_t b) { return b ? "TRUE" : "FALSE"; }
 
-void text_msg(Out& o, uint64_t k) {
+void text_msg(Out& o, uint64_t k, const int* pi = nullptr) {
   static const char* TN[4] = {"RequestVoteRequest", "RequestVoteResponse", "AppendEntriesRequest",
                               "AppendEntriesResponse"};
   o.s("[mtype |-> \"");
@@ -145,9 +146,9 @@ void text_msg(Out& o, uint64_t k) {
       break;
   }
   o.s("msource |-> ");
-  o.srv(m_src(k));
+  o.srv(pi ? (uint32_t)pi[m_src(k)] : m_src(k));
   o.s(", mdest |-> ");
-  o.srv(m_dst(k));
+  o.srv(pi ? (uint32_t)pi[m_dst(k)] : m_dst(k));
   o.c(']');
 }
 
@@ -195,95 +196,245 @@ size_t text_cap(const Layout& L) {
          (size_t)L.n_logs * (log + 2) + (size_t)L.N * (400 + log + 2 * vl + 40 * L.N);
 }
 
-}  // namespace
+// A row decoded once; the text of any server-permuted image pi(s) is
+// rendered from it (pi relabels every server-valued field, sg = pi^-1 gives
+// the server whose record lands at each position; nullptr = the state).
+struct Dec {
+  int N, nm, ne;
+  uint32_t rec[NMAX][3 + NMAX];
+  uint64_t key[KMAX];
+  uint32_t cnt[KMAX];
+  uint32_t er[EMAX][2 + NMAX];
+};
 
-size_t state_text_cap(const Layout& L) { return text_cap(L); }
-
-size_t state_text_into(const Layout& L, const uint32_t* row, char* buf, char* scratch) {
-  const int N = L.N;
-  Out o{buf};
-  Items it;
-  it.scratch.p = scratch;
-  const int nm = row_nmsg(L, row);
-  for (int k = 0; k < nm; k++) {
+void decode(const Layout& L, const uint32_t* row, Dec& d) {
+  d.N = L.N;
+  d.nm = row_nmsg(L, row);
+  d.ne = row_nelec(L, row);
+  for (int i = 0; i < L.N; i++) srv_get(L, row, i, d.rec[i]);
+  for (int k = 0; k < d.nm; k++) {
     const uint64_t v = bag_slot(L, row, k);
+    d.key[k] = m_key(v);
+    d.cnt[k] = m_count(v);
+  }
+  for (int e = 0; e < d.ne; e++) elec_get(L, row, e, d.er[e]);
+}
+
+uint32_t pmask(uint32_t m, const int* pi, int N) {  // {pi[j] : j \in m}
+  if (!pi) return m;
+  uint32_t r = 0;
+  for (int j = 0; j < N; j++)
+    if (m >> j & 1u) r |= 1u << pi[j];
+  return r;
+}
+
+void line_messages(Out& o, Items& it, const Dec& d, const int* pi) {
+  for (int k = 0; k < d.nm; k++) {
     it.begin();
-    text_msg(it.scratch, m_key(v));
+    text_msg(it.scratch, d.key[k], pi);
     it.scratch.s(" :> ");
-    it.scratch.u(m_count(v));
+    it.scratch.u(d.cnt[k]);
     it.end();
   }
   o.s("/\\ messages = ");
   it.emit(o, "(", " @@ ", ")", "<<>>");
-  const int ne = row_nelec(L, row);
-  for (int e = 0; e < ne; e++) {
-    uint32_t r[2 + NMAX];
-    elec_get(L, row, e, r);
+}
+
+void line_elections(Out& o, Items& it, const Dec& d, const int* pi) {
+  const int N = d.N;
+  for (int e = 0; e < d.ne; e++) {
+    const uint32_t* r = d.er[e];
     const uint32_t w0 = r[0];
+    uint32_t vl[NMAX];
+    for (int j = 0; j < N; j++) vl[pi ? pi[j] : j] = r[2 + j];
     Out& s = it.scratch;
     it.begin();
     s.s("[eterm |-> ");
     s.u(w0 & 15u);
     s.s(", eleader |-> ");
-    s.srv((w0 >> 4) & 7u);
+    const uint32_t ld = (w0 >> 4) & 7u;
+    s.srv(pi ? (uint32_t)pi[ld] : ld);
     s.s(", elog |-> ");
     text_log(s, r[1]);
     s.s(", evotes |-> ");
-    text_srvset(s, (w0 >> 7) & 31u, N);
+    text_srvset(s, pmask((w0 >> 7) & 31u, pi, N), N);
     s.s(", evoterLog |-> ");
-    text_vl(s, (w0 >> 12) & 31u, r + 2, N);
+    text_vl(s, pmask((w0 >> 12) & 31u, pi, N), vl, N);
     s.c(']');
     it.end();
   }
-  o.s("\n/\\ elections = ");
+  o.s("/\\ elections = ");
   it.emit(o, "{", ", ", "}", "{}");
+}
+
+void line_alllogs(Out& o, Items& it, const Layout& L, const uint32_t* row) {
   for (int x = 0; x < L.n_logs; x++)
     if (row[L.off_all + (x >> 5)] >> (x & 31) & 1u) {
       it.begin();
       text_log(it.scratch, log_from_index(L, x));
       it.end();
     }
-  o.s("\n/\\ allLogs = ");
+  o.s("/\\ allLogs = ");
   it.emit(o, "{", ", ", "}", "{}");
-  uint32_t recs[NMAX][3 + NMAX];  // the server records, unpacked
-  for (int i = 0; i < N; i++) srv_get(L, row, i, recs[i]);
-  auto per = [&](const char* name, auto fn) {
-    o.s("\n/\\ ");
-    o.s(name);
-    o.s(" = (");
-    for (int i = 0; i < N; i++) {
-      if (i) o.s(" @@ ");
-      o.srv((uint32_t)i);
-      o.s(" :> ");
-      fn(recs[i]);
-    }
-    o.c(')');
-  };
+}
+
+// The k-th per-server line (raft.tla:50-85 order): currentTerm, state,
+// votedFor, log, commitIndex, votesResponded, votesGranted, voterLog,
+// nextIndex, matchIndex.
+constexpr int SRV_LINES = 10;
+void line_server(Out& o, const Dec& d, int k, const int* pi, const int* sg) {
+  static const char* NAME[SRV_LINES] = {"currentTerm", "state", "votedFor", "log", "commitIndex",
+                                        "votesResponded", "votesGranted", "voterLog", "nextIndex", "matchIndex"};
   static const char* RN[4] = {"\"Follower\"", "\"Candidate\"", "\"Leader\"", "\"?\""};
-  per("currentTerm", [&](const uint32_t* r) { o.u(s_term(r[0])); });
-  per("state", [&](const uint32_t* r) { o.s(RN[s_role(r[0])]); });
-  per("votedFor", [&](const uint32_t* r) {
-    if (s_voted(r[0]) == NIL) o.s("\"Nil\"");
-    else o.srv(s_voted(r[0]));
-  });
-  per("log", [&](const uint32_t* r) { text_log(o, r[1]); });
-  per("commitIndex", [&](const uint32_t* r) { o.u(s_commit(r[0])); });
-  per("votesResponded", [&](const uint32_t* r) { text_srvset(o, s_vresp(r[0]), N); });
-  per("votesGranted", [&](const uint32_t* r) { text_srvset(o, s_vgrant(r[0]), N); });
-  per("voterLog", [&](const uint32_t* r) { text_vl(o, s_vlp(r[0]), r + 3, N); });
-  auto idx = [&](const uint32_t* r, bool match) {
-    o.c('(');
-    for (int j = 0; j < N; j++) {
-      if (j) o.s(" @@ ");
-      o.srv((uint32_t)j);
-      o.s(" :> ");
-      o.u(match ? nm_match(r[2], j) : nm_next(r[2], j));
+  const int N = d.N;
+  o.s("/\\ ");
+  o.s(NAME[k]);
+  o.s(" = (");
+  for (int p = 0; p < N; p++) {
+    const uint32_t* r = d.rec[sg ? sg[p] : p];
+    if (p) o.s(" @@ ");
+    o.srv((uint32_t)p);
+    o.s(" :> ");
+    switch (k) {
+      case 0: o.u(s_term(r[0])); break;
+      case 1: o.s(RN[s_role(r[0])]); break;
+      case 2:
+        if (s_voted(r[0]) == NIL) o.s("\"Nil\"");
+        else o.srv(pi ? (uint32_t)pi[s_voted(r[0])] : s_voted(r[0]));
+        break;
+      case 3: text_log(o, r[1]); break;
+      case 4: o.u(s_commit(r[0])); break;
+      case 5: text_srvset(o, pmask(s_vresp(r[0]), pi, N), N); break;
+      case 6: text_srvset(o, pmask(s_vgrant(r[0]), pi, N), N); break;
+      case 7: {
+        uint32_t vl[NMAX];
+        for (int q = 0; q < N; q++) vl[q] = r[3 + (sg ? sg[q] : q)];
+        text_vl(o, pmask(s_vlp(r[0]), pi, N), vl, N);
+        break;
+      }
+      default: {
+        o.c('(');
+        for (int q = 0; q < N; q++) {
+          if (q) o.s(" @@ ");
+          o.srv((uint32_t)q);
+          o.s(" :> ");
+          const int j = sg ? sg[q] : q;
+          o.u(k == 8 ? nm_next(r[2], j) : nm_match(r[2], j));
+        }
+        o.c(')');
+      }
     }
-    o.c(')');
-  };
-  per("nextIndex", [&](const uint32_t* r) { idx(r, false); });
-  per("matchIndex", [&](const uint32_t* r) { idx(r, true); });
+  }
+  o.c(')');
+}
+
+// The text of the image pi(s), lines in TLC order.
+size_t image_text(const Layout& L, const uint32_t* row, const Dec& d, const int* pi, const int* sg, char* buf,
+                  char* scratch) {
+  Out o{buf};
+  Items it;
+  it.scratch.p = scratch;
+  line_messages(o, it, d, pi);
+  o.c('\n');
+  line_elections(o, it, d, pi);
+  o.c('\n');
+  line_alllogs(o, it, L, row);
+  for (int k = 0; k < SRV_LINES; k++) {
+    o.c('\n');
+    line_server(o, d, k, pi, sg);
+  }
   return o.n;
+}
+
+}  // namespace
+
+size_t state_text_cap(const Layout& L) { return text_cap(L); }
+
+size_t state_text_into(const Layout& L, const uint32_t* row, char* buf, char* scratch) {
+  Dec d;
+  decode(L, row, d);
+  return image_text(L, row, d, nullptr, nullptr, buf, scratch);
+}
+
+// The orbit text (the per-orbit item of a SYMMETRY level's digest,
+// DESIGN.md section 3): the text of the image pi(s) whose ROTATED text --
+// the ten per-server lines first, then messages, elections, allLogs -- is
+// least over all N! permutations.  Defined on the value text alone, so the
+// CPU oracle (oracle/raft_cpu.c orbit_text) and the value oracle compute it
+// independently of this code; nothing here uses the kernels' orbit key.
+//
+// The images are compared line by line, each dropped at its first line
+// above the best so far.  One exact shortcut: the first two rotated lines
+// (currentTerm, state) print a relabel-free token per position (a decimal
+// term, a quoted role; neither token set has one token a proper prefix of
+// another followed by a character that sorts below the delimiters " @@ " /
+// ")"), so their least text lists the servers sorted by (term text, role
+// text), and every image that does not is above it there: only the
+// orderings within ties of (term, role) are rendered.
+size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, char* scratch) {
+  Dec d;
+  decode(L, row, d);
+  const int N = d.N;
+  // servers sorted by (term text, role text): the key packs the term's
+  // decimal text (two digits, a one-digit term's second digit below '0')
+  // and the role's rank in text order ("Candidate" < "Follower" < "Leader")
+  static const int RRANK[4] = {1, 0, 2, 3};
+  int key[NMAX];
+  for (int i = 0; i < N; i++) {
+    const uint32_t t = s_term(d.rec[i][0]);
+    const int d0 = t >= 10 ? (int)(t / 10) : (int)t, d1 = t >= 10 ? (int)(t % 10) : -1;
+    key[i] = (d0 * 11 + (d1 + 1)) * 4 + RRANK[s_role(d.rec[i][0])];
+  }
+  int sg[NMAX], pi[NMAX], best_sg[NMAX];
+  for (int i = 0; i < N; i++) sg[i] = i;
+  std::stable_sort(sg, sg + N, [&](int a, int b) { return key[a] < key[b]; });
+  int gb[NMAX + 1], ng = 0;  // tie groups [gb[g], gb[g+1]) of positions
+  for (int p = 0; p < N; p++)
+    if (p == 0 || key[sg[p]] != key[sg[p - 1]]) gb[ng++] = p;
+  gb[ng] = N;
+  // rotated text minus the first two lines (equal for every candidate),
+  // compared line by line with the best so far
+  const size_t cap = text_cap(L);
+  thread_local std::vector<char> work;  // two rotated texts (candidate, best)
+  if (work.size() < 2 * cap) work.resize(2 * cap);
+  char* bufs[2] = {work.data(), work.data() + cap};
+  int bi = -1;
+  size_t bn = 0;
+  Items it;
+  it.scratch.p = scratch;
+  for (;;) {
+    for (int p = 0; p < N; p++) pi[sg[p]] = p;
+    const int ci = bi < 0 ? 0 : bi ^ 1;
+    Out o{bufs[ci]};
+    bool below = bi < 0, above = false;
+    auto cmp_line = [&](size_t from) {  // the line just written: below / above / equal to best's bytes
+      if (below) return;
+      const int r = memcmp(o.p + from, bufs[bi] + from, o.n - from);
+      if (r < 0) below = true;
+      else if (r > 0) above = true;
+    };
+    for (int k = 2; k < SRV_LINES + 3 && !above; k++) {
+      const size_t from = o.n;
+      o.c('\n');
+      if (k < SRV_LINES) line_server(o, d, k, pi, sg);
+      else if (k == SRV_LINES) line_messages(o, it, d, pi);
+      else if (k == SRV_LINES + 1) line_elections(o, it, d, pi);
+      else line_alllogs(o, it, L, row);
+      cmp_line(from);
+    }
+    if (below) {
+      bi = ci;
+      bn = o.n;
+      for (int p = 0; p < N; p++) best_sg[p] = sg[p];
+    }
+    // next ordering: an odometer over the tie groups' permutations
+    int g = ng - 1;
+    while (g >= 0 && !std::next_permutation(sg + gb[g], sg + gb[g + 1])) g--;
+    if (g < 0) break;
+  }
+  (void)bn;
+  for (int p = 0; p < N; p++) pi[best_sg[p]] = p;
+  return image_text(L, row, d, pi, best_sg, buf, scratch);
 }
 
 std::string state_text(const Layout& L, const uint32_t* row) {

@@ -15,6 +15,8 @@ std::string state_text(const Layout& L, const uint32_t* row);
 // again, for the items of the sorted collections); returns its length.
 size_t state_text_cap(const Layout& L);
 size_t state_text_into(const Layout& L, const uint32_t* row, char* buf, char* scratch);
+// SYMMETRY: the orbit text of the state (rtla_text.cpp; the same buffers).
+size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, char* scratch);
 // Human-readable label of an action instance (+ Receive sub-action).
 std::string action_name(const Layout& L, int inst, int sub);
 

@@ -83,6 +83,10 @@ def _load():
         "rtla_recover": (C.c_int, [C.c_void_p, C.c_char_p]),
         "rtla_probe_bench2": (C.c_int, [C.c_int, C.c_uint64, P(C.c_double), P(C.c_double), P(C.c_double),
                                         P(C.c_uint64)]),
+        "rtla_probe_bench3": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_double, P(C.c_double),
+                                        P(C.c_uint64)]),
+        "rtla_random_texts": (C.c_int, [P(_Cfg), C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_char_p,
+                                        C.c_size_t, P(C.c_size_t)]),
         "rtla_row_words": (C.c_int, [P(_Cfg)]),
         "rtla_row_layout": (C.c_int, [P(_Cfg), P(C.c_int32), C.c_int]),
         "rtla_init_row": (C.c_int, [P(_Cfg), P(C.c_uint32)]),
@@ -104,6 +108,9 @@ def _load():
         "rtla_permute_row": (C.c_int, [P(_Cfg), P(C.c_uint32), P(C.c_int), P(C.c_uint32)]),
         "rtla_rows_text_hash": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, C.c_int, P(C.c_uint64)]),
         "rtla_level_text_hash": (C.c_int, [C.c_void_p, C.c_int, P(C.c_uint64)]),
+        "rtla_rows_orbit_hash": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_size_t, C.c_int, P(C.c_uint64)]),
+        "rtla_level_orbit_hash": (C.c_int, [C.c_void_p, C.c_int, P(C.c_uint64)]),
+        "rtla_orbit_text": (C.c_int, [P(_Cfg), P(C.c_uint32), C.c_char_p, C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -120,7 +127,8 @@ EXPORTED = ["rtla_open", "rtla_close", "rtla_comm_id", "rtla_init", "rtla_reset"
             "rtla_strerror", "rtla_abi_version", "rtla_probe_bench", "rtla_time_expand",
             "rtla_probe_bench2", "rtla_checkpoint", "rtla_recover", "rtla_random_rows", "rtla_synthetic_step",
             "rtla_synthetic_generate", "rtla_synthetic_dedup", "rtla_orbit_key", "rtla_permute_row",
-            "rtla_rows_text_hash", "rtla_level_text_hash", "rtla_row_layout"]
+            "rtla_rows_text_hash", "rtla_level_text_hash", "rtla_row_layout", "rtla_rows_orbit_hash",
+            "rtla_level_orbit_hash", "rtla_orbit_text", "rtla_probe_bench3", "rtla_random_texts"]
 
 SYNTH_SEED = 0x5AF72025  # the synthetic microbench's PRNG seed
 
@@ -285,6 +293,50 @@ def rows_text_hash(cfg: Config, rows: Sequence[Sequence[int]], threads: int = 0)
     return out.value
 
 
+def rows_orbit_hash(cfg: Config, rows: Sequence[Sequence[int]], threads: int = 0) -> int:
+    """Sum mod 2^64 of FNV-1a-64 of each row's ORBIT TEXT (rtla_rows_orbit_hash):
+    a SYMMETRY level's digest, whichever member of each orbit a row holds."""
+    cc = cfg.c()
+    w = row_words(cfg)
+    n = len(rows)
+    flat = (C.c_uint32 * max(1, n * w))()
+    for k, r in enumerate(rows):
+        flat[k * w:(k + 1) * w] = list(r)
+    out = C.c_uint64(0)
+    _check(_lib.rtla_rows_orbit_hash(C.byref(cc), flat, n, threads, C.byref(out)), "rtla_rows_orbit_hash")
+    return out.value
+
+
+def orbit_text(cfg: Config, row: Sequence[int]) -> str:
+    """The text of the orbit representative whose rotated text is least
+    (rtla_orbit_text; the item of a SYMMETRY level digest)."""
+    cc = cfg.c()
+    arr = (C.c_uint32 * len(row))(*row)
+    cap = 1 << 16
+    while True:
+        buf = C.create_string_buffer(cap)
+        st = _lib.rtla_orbit_text(C.byref(cc), arr, buf, cap)
+        if st >= 0:
+            return buf.value.decode()
+        cap *= 4
+        if cap > 1 << 26:
+            raise RtlaError(st, "rtla_orbit_text")
+
+
+def random_texts(cfg: Config, first: int, n: int, pool: int = 0, seed: int = SYNTH_SEED) -> bytes:
+    """The synthetic input states first .. first + n - 1 as state texts, each
+    terminated by '\x1e' (rtla_random_texts; host)."""
+    cc = cfg.c()
+    need = C.c_size_t(0)
+    cap = n * 8192
+    buf = C.create_string_buffer(cap)
+    if _lib.rtla_random_texts(C.byref(cc), seed, first, n, pool, buf, cap, C.byref(need)) != OK:
+        buf = C.create_string_buffer(need.value + 1)
+        _check(_lib.rtla_random_texts(C.byref(cc), seed, first, n, pool, buf, need.value, C.byref(need)),
+               "rtla_random_texts")
+    return buf.raw[:need.value]
+
+
 def stored_fingerprint(row: Sequence[int]):
     return row[0] | row[1] << 32, row[2] | row[3] << 32
 
@@ -435,6 +487,13 @@ class Checker:
         _check(_lib.rtla_level_text_hash(self._h, threads, C.byref(out)), "rtla_level_text_hash")
         return out.value
 
+    def level_orbit_hash(self, threads: int = 0) -> int:
+        """SYMMETRY: the level's digest over orbit texts (rtla_level_orbit_hash),
+        compared with the oracle's per-level orbit digest."""
+        out = C.c_uint64(0)
+        _check(_lib.rtla_level_orbit_hash(self._h, threads, C.byref(out)), "rtla_level_orbit_hash")
+        return out.value
+
     def checkpoint(self, prefix: str):
         """TLC -checkpoint: write the search to <prefix>.shard<id>.rtla (between levels)."""
         _check(_lib.rtla_checkpoint(self._h, prefix.encode()), "rtla_checkpoint")
@@ -508,6 +567,14 @@ def probe_bench2(log2: int, n: int):
     a, b, c, ins = C.c_double(0), C.c_double(0), C.c_double(0), C.c_uint64(0)
     _check(_lib.rtla_probe_bench2(log2, n, C.byref(a), C.byref(b), C.byref(c), C.byref(ins)), "rtla_probe_bench2")
     return a.value, b.value, c.value, ins.value
+
+
+def probe_mixed(log2: int, n_present: int, n: int, new_frac: float):
+    """(seconds, inserted): n load-first probes into a 2^log2 table holding
+    n_present keys, a fraction new_frac of them new keys (rtla_probe_bench3)."""
+    sec, ins = C.c_double(0), C.c_uint64(0)
+    _check(_lib.rtla_probe_bench3(log2, n_present, n, new_frac, C.byref(sec), C.byref(ins)), "rtla_probe_bench3")
+    return sec.value, ins.value
 
 
 def probe_bench(log2: int, n: int):

@@ -6,7 +6,7 @@ and the two must agree on every level's counts and state-text hash before the
 case is written.  The configs are the build's bounded models (specs/MC.tla);
 the reference ships no fixtures of its own.
 
-    python tests/golden/make_golden.py [--big]
+    python tests/golden/make_golden.py [--big] [--only=name,name]
 """
 import json
 import os
@@ -58,13 +58,14 @@ PREFIXES = {
     # BASELINE.json configs[2] as stated (2 copies per message: Duplicate/Drop live)
     "n3_v2_t4_l3_c2_prefix": (3, 2, 4, 3, 2, 0, (), 0, 14),
 }
-# SYMMETRY prefixes (orbit counts per level; no text hashes: the orbit
-# representatives kept differ between implementations).  N = 4 and BASELINE
-# configs[3] (N = 5) as stated.
+# SYMMETRY prefixes: orbit counts and orbit-text digests per level (the
+# orbit text is the same whichever member of an orbit an implementation
+# keeps).  N = 4, and BASELINE configs[3] (N = 5) as stated to the 15 levels
+# bench.py times.
 # name: (N, V, T, L, C, M, invariants, max_distinct, max_levels)
 SYM_PREFIXES = {
     "n4_v1_t2_l1_m1_sym_prefix": (4, 1, 2, 1, 1, 1, (NTL,), 3_000_000, 0),
-    "n5_v1_t3_l2_c1_sym_prefix": (5, 1, 3, 2, 1, 0, (), 3_000_000, 0),
+    "n5_v1_t3_l2_c1_sym_prefix": (5, 1, 3, 2, 1, 0, (), 0, 15),
 }
 
 
@@ -101,16 +102,20 @@ def main():
         if (is_big and not big) or (only and name not in only):
             continue
         cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, symmetry=True)
-        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, keep_trace=not is_big, text_hash=True)
         assert r["rc"] >= 0, (name, r["rc"])
         case = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
                 "invariants": list(inv), "symmetry": True, "distinct": r["distinct"], "generated": r["generated"],
                 "depth": r["depth"], "levels": r["levels"], "violated": r["violated"], "trace_len": r["trace_len"],
-                "source": "oracle/raft_cpu.c (orbit key: least serialisation over server permutations)"}
+                "level_orbit_hash": ["%016x" % h for h in r["level_text_hash"]],
+                "source": "oracle/raft_cpu.c (orbit key: least orbit serialisation over server permutations; "
+                          "level_orbit_hash: sum of FNV-1a of each new orbit's orbit text)"}
         if py and not r["violated"]:
-            pl = rv.bfs_symmetric(rv.Cfg(n, v, t, l, c, inv, m))
+            ph = []
+            pl = rv.bfs_symmetric(rv.Cfg(n, v, t, l, c, inv, m), ph)
             assert [list(x) for x in pl] == r["levels"], name
-            case["source"] += " + oracle/raft_values.py (orbit key: least text over permutations)"
+            assert ph == r["level_text_hash"], name
+            case["source"] += " + oracle/raft_values.py (orbit key: least text over permutations; orbit texts)"
         out[name] = case
         print(name, r["distinct"], r["generated"], r["depth"], r["violated"], "%.1fs" % r["seconds"], flush=True)
     for name, (n, v, t, l, c, m, inv, cap, depth) in PREFIXES.items():
@@ -133,14 +138,17 @@ def main():
             continue
         cfg = raft_cpu.cfg_of(n, v, t, l, c, m, inv, max_distinct=cap, symmetry=True, max_levels=depth)
         cfg.verbose = 1
-        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8)
+        r = raft_cpu.bfs(cfg, threads=os.cpu_count() or 8, text_hash=True)
         assert r["rc"] in (0, -4), (name, r["rc"])
         out[name] = {"n_server": n, "n_value": v, "max_term": t, "max_log": l, "max_copies": c, "max_msgs": m,
                      "invariants": list(inv), "prefix": True, "symmetry": True, "levels": r["levels"],
                      "distinct": r["distinct"], "generated": r["generated"], "max_msgs_seen": r["max_msgs"],
-                     "source": "oracle/raft_cpu.c (orbit key: least serialisation over server permutations), "
-                               "first %d complete levels" % len(r["levels"])}
+                     "level_orbit_hash": ["%016x" % h for h in r["level_text_hash"]],
+                     "source": "oracle/raft_cpu.c (orbit key: least orbit serialisation over server permutations; "
+                               "level_orbit_hash: orbit texts), first %d complete levels" % len(r["levels"])}
         print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

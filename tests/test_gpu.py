@@ -23,7 +23,17 @@ pytestmark = pytest.mark.gpu
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bfs_counts.json")))
 SMALL = sorted(k for k, v in GOLD.items() if v["distinct"] < 3_000_000 and not v.get("prefix"))
-HASHED = sorted(k for k in SMALL if "level_text_hash" in GOLD[k])
+HASHED = sorted(k for k in SMALL if "level_text_hash" in GOLD[k] or "level_orbit_hash" in GOLD[k])
+
+
+def level_digests(g):
+    """The fixture's per-level content digests and the checker's matching
+    method: state texts, or (SYMMETRY) orbit texts -- the text of the image
+    whose rotated text is least over all server permutations, the same for
+    whichever member of an orbit the GPU or the oracle keeps."""
+    if g.get("symmetry"):
+        return g.get("level_orbit_hash", []), lambda ck: ck.level_orbit_hash()
+    return g.get("level_text_hash", []), lambda ck: ck.level_text_hash()
 
 
 def cfg_of(g, **kw):
@@ -50,16 +60,17 @@ def test_bfs_counts_match_golden(name):
 def test_level_contents_match_oracle(name):
     g = GOLD[name]
     cfg = cfg_of(g, **small_kw(g))
+    want, digest = level_digests(g)
     got = []
     with rtla.Checker(cfg) as ck:
         st = ck.init()
         while True:
-            got.append("%016x" % ck.level_text_hash())
-            if st != rtla.OK or len(got) >= len(g["level_text_hash"]):
+            got.append("%016x" % digest(ck))
+            if st != rtla.OK or len(got) >= len(want):
                 break
             st = ck.step()
-    n = min(len(got), len(g["level_text_hash"]))
-    assert got[:n] == g["level_text_hash"][:n]
+    n = min(len(got), len(want))
+    assert n >= len(want) - 1 and got[:n] == want[:n]
 
 
 WALKS = [(2, 2, 3, 2, 1, 1), (3, 1, 2, 1, 1, 2), (3, 2, 3, 2, 1, 3), (3, 2, 4, 3, 2, 4),
@@ -87,6 +98,46 @@ def test_lockstep_walk_successors_match_oracle(shape):
         text = rtla.state_text(cfg, row)
         walk.goto(text)
         assert rtla.invariants_violated(cfg, row) == walk.invariants()
+
+
+@pytest.mark.parametrize("shape", [(5, 1, 3, 2, 1, 0), (4, 1, 2, 1, 1, 2), (3, 2, 3, 2, 1, 3)])
+def test_symmetric_lockstep_walk_orbit_keys_match_oracle(shape):
+    """SYMMETRY at the successor level, N = 5 (BASELINE configs[3]'s shape)
+    included: along a random walk, the successors the GPU generates
+    (rtla_expand_batch runs the level kernel) are grouped into orbits by the
+    product's orbit key (rtla_model.h sym_key, the seen-set key the kernel
+    probes) exactly as the C oracle groups them by its least orbit
+    serialisation over all N! permutations; and each successor's orbit text
+    (rtla_orbit_text) equals the oracle's."""
+    n, v, t, l, c, m = shape
+    cfg = rtla.Config(n, v, t, l, c, m, (), symmetry=True, bag_cap=20)
+    walk = raft_cpu.Walk(raft_cpu.cfg_of(n, v, t, l, c, m, (), symmetry=True))
+    rnd = random.Random(sum(shape))
+    row = rtla.init_row(cfg)
+    checked = 0
+    for step in range(60):
+        gpu = [x for x in rtla.expand_batch(cfg, [row]) if x[3]]
+        texts = walk.successors()
+        orbits = walk.orbits()          # (oracle key, orbit text) per successor, in texts' order
+        ref = {}
+        for (im, tx), (okey, otext) in zip(texts, orbits):
+            if im:
+                ref[tx] = (okey, otext)
+        mine_key, mine_orb = {}, {}
+        for x in gpu:
+            tx = rtla.state_text(cfg, x[4])
+            okey, otext = ref[tx]
+            assert rtla.orbit_text(cfg, x[4]) == otext, "step %d" % step
+            mine_key.setdefault(rtla.orbit_key(cfg, x[4])[0], set()).add(okey)
+            mine_orb.setdefault(okey, set()).add(rtla.orbit_key(cfg, x[4])[0])
+            checked += 1
+        # the two partitions of the successors into orbits coincide
+        assert all(len(v) == 1 for v in mine_key.values()) and all(len(v) == 1 for v in mine_orb.values())
+        if not gpu:
+            break
+        row = rnd.choice(gpu)[4]
+        walk.goto(rtla.state_text(cfg, row))
+    assert checked > 200
 
 
 def test_incremental_fingerprint_equals_full_rehash():
@@ -171,13 +222,13 @@ def test_full_size_counts_match_golden(name):
     the decoded GPU rows, rtla_level_text_hash, against the oracle's)."""
     g = GOLD[name]
     cfg = cfg_of(g, fpset_log2=(g["distinct"] * 3).bit_length())
-    hashes = g.get("level_text_hash", [])
+    hashes, digest = level_digests(g)
     with rtla.Checker(cfg) as ck:
         st = ck.init()
         while True:
             k = len(ck.levels) - 1
-            if k < len(hashes) and not g.get("symmetry"):
-                assert "%016x" % ck.level_text_hash() == hashes[k], "level %d" % (k + 1)
+            if k < len(hashes):
+                assert "%016x" % digest(ck) == hashes[k], "level %d" % (k + 1)
             if st != rtla.OK:
                 break
             st = ck.step()
@@ -212,17 +263,18 @@ def test_prefix_levels_match_golden(name):
     """Models too large for the CPU oracle to exhaust -- BASELINE configs[0],
     [1] and [2] exactly as stated, to the depth bench.py times them at, the
     exhaust model's first 31 levels, and the SYMMETRY prefixes: per-level
-    counts, and (non-symmetric) the set of states of EVERY level: the level
-    digest of the decoded GPU rows against the oracle's."""
+    counts, and the contents of EVERY level: the level digest of the decoded
+    GPU rows (SYMMETRY: of their orbit texts -- configs[3] to the 15 levels
+    bench.py times) against the oracle's."""
     g = GOLD[name]
     cfg = cfg_of(g, fpset_log2=max(30, (g["distinct"] * 3).bit_length()), bag_cap=PREFIX_BAG.get(name, 0))
-    hashes = g.get("level_text_hash", [])
+    hashes, digest = level_digests(g)
     with rtla.Checker(cfg) as ck:
         st = ck.init()
         while True:
             k = len(ck.levels) - 1
             if k < len(hashes):
-                assert "%016x" % ck.level_text_hash() == hashes[k], "level %d" % (k + 1)
+                assert "%016x" % digest(ck) == hashes[k], "level %d" % (k + 1)
             if len(ck.levels) >= len(g["levels"]):
                 break
             assert st == rtla.OK
@@ -264,6 +316,25 @@ def test_virtual_shards_match_golden(name, shards):
     res = rtla.check(cfg_of(g, shards=shards, chunk=512, **kw), trace=False)
     assert [[lv.new, lv.generated] for lv in res.levels] == g["levels"]
     assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
+
+
+@pytest.mark.parametrize("name", ["n3_v1_t2_l1_m2", "n3_v1_t2_l1_m2_sym"])
+def test_many_shards_tiny_sent_cache_match_golden(name):
+    """8 fingerprint-owned shards whose sent caches (2^(fpset_log2 - 2)
+    slots, overwritten on a miss) are far smaller than the millions of
+    fingerprints each ships: duplicates are re-sent and deduplicated by the
+    owners -- the counts stay exact, and no capacity error is raised (the
+    overwrite-on-miss cache has no probe chain to run out of).  Also checks
+    that the level-end re-balancing kept the shards' levels within 2 % of an
+    even split."""
+    g = GOLD[name]
+    fpl = (g["distinct"] * 2).bit_length() - 3   # per shard: ~30-40 % load over the 8 shards
+    cfg = cfg_of(g, shards=8, chunk=4096, fpset_log2=fpl, mem_budget=24 << 30)
+    with rtla.Checker(cfg) as ck:
+        assert ck.run() == rtla.DONE
+        info = json.loads(ck.device_info())
+        assert info["sent_cache_slots_log2"] == fpl - 2 and info["rebalanced_rows"] > 0
+        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
 
 
 @pytest.mark.parametrize("shards", [2, 3, 8])

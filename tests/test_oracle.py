@@ -148,3 +148,32 @@ def test_symmetry_orbit_keys_are_permutation_invariant():
     for s in some:
         for pi in itertools.permutations(range(2)):
             assert rv.orbit_key(cfg, rv.permute_state(s, pi)) == rv.orbit_key(cfg, s)
+
+
+@pytest.mark.parametrize("shape", [(3, 1, 3, 2, 1, 0), (4, 1, 2, 1, 1, 2)])
+def test_walk_orbit_texts_match_value_oracle(shape):
+    """The C oracle's per-successor orbit texts (its early-exit minimum over
+    all N! images) equal the value oracle's brute force, and its seen-set key
+    (least orbit serialisation) groups the successors into the same orbits as
+    the value oracle's least text over permutations."""
+    import random
+    import tla_text
+    n, v, t, l, c, m = shape
+    vc = rv.Cfg(n, v, t, l, c, (), m)
+    w = raft_cpu.Walk(raft_cpu.cfg_of(n, v, t, l, c, m, (), symmetry=True))
+    rnd = random.Random(7)
+    for _ in range(25):
+        succ = w.successors()
+        orb = w.orbits()
+        assert len(orb) == len(succ)
+        by_key = {}
+        for (im, tx), (key, otext) in zip(succ, orb):
+            s = tla_text.parse_state(vc, tx)
+            assert otext == rv.orbit_text(vc, s)
+            by_key.setdefault(key, set()).add(rv.orbit_key(vc, s))
+        assert all(len(x) == 1 for x in by_key.values())
+        assert len(by_key) == len({k for x in by_key.values() for k in x})
+        inm = [tx for im, tx in succ if im]
+        if not inm:
+            break
+        w.goto(rnd.choice(inm))

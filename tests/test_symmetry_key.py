@@ -82,3 +82,33 @@ def test_permute_row_keeps_state_validity():
         assert back == r
     with pytest.raises(rtla.RtlaError):
         rtla.permute_row(cfg, r, [0, 0, 1])
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5])
+def test_orbit_text_matches_value_oracle(n):
+    """The SYMMETRY level digest's per-orbit item (rtla_orbit_text, host C++
+    over the packed row, with its exact shortcut on the first two rotated
+    lines) equals the value oracle's brute force over every permutation
+    (raft_values.orbit_text on the parsed state), is the same for every
+    image of a state, and rtla_rows_orbit_hash sums FNV-1a of exactly these
+    texts."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import raft_values as rv
+    import tla_text
+    cfg = cfg_of(n)
+    vc = rv.Cfg(n, 1, cfg.max_term, cfg.max_log, 1, (), 0)
+    all_perms = [list(p) for p in itertools.permutations(range(n))]
+    rng = random.Random(100 + n)
+    base = rtla.random_rows(cfg, 0, 24 if n < 5 else 8, pool=0)
+    rows = base + [look_alike(cfg, r, rng.randrange(1, n)) for r in base[:8]] + [rtla.init_row(cfg)]
+    rows += [rtla.permute_row(cfg, r, rng.choice(all_perms)) for r in rows[:10]]
+    texts = []
+    for r in rows:
+        t = rtla.orbit_text(cfg, r)
+        assert t == rv.orbit_text(vc, tla_text.parse_state(vc, rtla.state_text(cfg, r)))
+        for pi in rng.sample(all_perms, min(len(all_perms), 6)):
+            assert rtla.orbit_text(cfg, rtla.permute_row(cfg, r, pi)) == t
+        texts.append(t)
+    assert rtla.rows_orbit_hash(cfg, rows, threads=2) == sum(rv.fnv1a64(t) for t in texts) & (2 ** 64 - 1)

@@ -40,3 +40,36 @@ def test_input_numbering_is_deterministic_with_pool_repeats():
     # ~half the inputs are fresh, the rest fall into 40 pool states
     assert 250 < distinct < 350, distinct
     assert rtla.random_rows(cfg, 0, 10, pool=40, seed=1) != a[:10]
+
+
+def test_oracle_dedup_of_random_texts_matches_value_oracle():
+    """The synthetic microbench's CPU leg: the C oracle parses the product's
+    random states from their text (rtla_random_texts) and runs Next + dedup;
+    its counts (generated, probes = in-model successors that differ from their
+    parent, new) equal the value oracle's over the same parsed states, across
+    two batches sharing one seen set."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import raft_cpu
+    import raft_values as rv
+    import tla_text
+    inv = ("ElectionSafety", "LogMatching")
+    cfg = rtla.Config(3, 2, 4, 3, 2, 0, inv, bag_cap=12)
+    vc = rv.Cfg(3, 2, 4, 3, 2, inv, 0)
+    n, pool = 120, 30
+    d = raft_cpu.Dedup(raft_cpu.cfg_of(3, 2, 4, 3, 2, 0, inv))
+    seen = set()
+    gen = probes = 0
+    for b in range(2):
+        blob = rtla.random_texts(cfg, b * n, n, pool)
+        texts = blob.decode().split("\x1e")[:-1]
+        assert len(texts) == n
+        for text in texts:
+            for _, t in rv.next_states(vc, tla_text.parse_state(vc, text)):
+                gen += 1
+                tt = rv.state_text(vc, t)
+                if rv.in_model(vc, t) and tt != text:
+                    probes += 1
+                    seen.add(tt)
+        assert d.batch(blob, n, threads=4) == [gen, probes, len(seen)]
