@@ -70,7 +70,7 @@ CAPPED = {"cfg1", "cfg2", "cfg3", "cfg4"}  # not exhaustible on one GPU
 # Complete levels of each capped workload that the CPU oracle pins (per-level
 # counts and state-set digests in tests/golden/bfs_counts.json): a timed step
 # runs exactly these (--depth fit: as many as device memory holds instead).
-PINNED_LEVELS = {"cfg1": 23, "cfg2": 17, "cfg3": 14}
+PINNED_LEVELS = {"cfg1": 23, "cfg2": 17, "cfg3": 14, "cfg4": 15}
 DEFAULT = "cfg2"
 SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run reports it too)
 # Fingerprint-set size (log2 slots) per workload: ~25-30 % load at the size reached.
