@@ -394,18 +394,23 @@ def roofline(levels, world, workload, calib=None):
     }
 
 
-def capacity(levels, info, fpl):
+def capacity(levels, info, fpl, parts=1):
     """What device memory holds beyond the timed levels: the frontier arena
     (current + next level share it), the fingerprint set's load, and whether
-    the next level -- estimated from the last level's growth -- would fit."""
+    the next level -- estimated from the last level's growth -- would fit.
+    Arena rows and set slots are per shard (rank or virtual shard); the
+    level counts are the job's, so they are split over the `parts` shards
+    (fingerprint ownership and the level-end re-balancing keep the shards
+    even)."""
     rows = info.get("frontier_cap") or 0
     last, prev = levels[-1].new, levels[-2].new if len(levels) > 1 else 1
     est_next = int(last * last / max(1, prev))
     distinct = sum(lv.new for lv in levels)
-    return {"arena_rows": rows, "row_bytes": levels[0].row_bytes, "fpset_slots_log2": fpl,
-            "fpset_load": distinct / float(1 << fpl), "last_level": last, "next_level_estimate": est_next,
-            "next_level_fits_arena": rows >= ((last + 63) // 64) * 64 + est_next,
-            "fpset_load_after_next": (distinct + est_next) / float(1 << fpl)}
+    per = lambda v: -(-v // max(1, parts))  # ceil(v / parts)
+    return {"arena_rows": rows, "row_bytes": levels[0].row_bytes, "fpset_slots_log2": fpl, "shards": parts,
+            "fpset_load": per(distinct) / float(1 << fpl), "last_level": last, "next_level_estimate": est_next,
+            "next_level_fits_arena": rows >= ((per(last) + 63) // 64) * 64 + per(est_next),
+            "fpset_load_after_next": per(distinct + est_next) / float(1 << fpl)}
 
 
 def synthetic(run, args, rank, world, barrier):
@@ -583,7 +588,7 @@ def main():
     if run.capped:
         config["stopped_by"] = run.stop
         config["oracle_pinned"] = bool(run.pinned) and not args.cap_levels
-        config["capacity"] = capacity(levels, info, run.fpl)
+        config["capacity"] = capacity(levels, info, run.fpl, max(1, world) * max(1, args.shards))
     out = {
         "metric": "distinct states/sec (whole node) + wall time to exhaust, 3-server Raft",
         "value": distinct / per_step,

@@ -81,6 +81,9 @@ enum {
   XF_ALL_SUCCESSORS = 16384,  // compact kernel: no seen set -- every enabled successor (in-model or not) gets a
                               // row, its record = input index << 32 | in_model << 31 | sub << 16 | instance
                               // (rtla_expand_batch: the parity seam runs the hot kernel)
+  XF_SYM_QUEUE = 32768,   // SYMMETRY, one shard (set by the driver): the compact kernel only evaluates and
+                          // queues (parent << 16 | instance) of the successors that need an orbit key into
+                          // box.send_ref[0, box.cap) (fill counter *box.out_count); k_sym_keys keys them
 };
 
 // Per-level device counters (zeroed before each level except `cover`).

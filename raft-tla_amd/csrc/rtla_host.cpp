@@ -96,6 +96,9 @@ struct Shard {
   uint64_t* sent = nullptr;        // [2^slog2] sent cache: fingerprints this shard already sent to their owners
   std::vector<uint64_t> h_out, h_in, h_all;
   uint64_t h_reb[2 * SHARD_MAX] = {};  // re-balancing: rows_in / rows_base of this sub-round (host staging)
+  // SYMMETRY, one shard: the key queue between the level kernel and k_sym_keys
+  uint64_t* queue = nullptr;        // [qcap] parent << 16 | instance (~0 = hole)
+  uint64_t* qcount = nullptr;       // its fill counter
   uint64_t h_caps[3] = {0, 0, 0};  // -> DevCounters cap_cur / cap_next / cap_parents
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   // violation found on this shard
@@ -137,6 +140,7 @@ struct rtla_ctx {
   int slog2 = 0;           // sent cache: 2^slog2 slots per shard (multi-shard)
   uint64_t front_cap = 0, box_cap = 0, chunk = 0, rows_cap = 0;
   uint64_t rebalanced = 0; // rows moved by level-end re-balancing (all levels, this process's shards)
+  uint64_t qcap = 0, qchunk = 0;  // SYMMETRY key queue: entries, frontier states per round (0: keys in the level kernel)
   uint64_t* red = nullptr;  // device scratch for all-reduces
   int level = 0;
   bool inited = false, finished = false;
@@ -760,7 +764,7 @@ extern "C" int rtla_comm_id(void* out128) {
 static void free_shard(Shard& s) {
   void* ptrs[] = {s.table,    s.sent,     s.parents,  s.arena,    s.ctr,       s.dflags,    s.out_count,
                   s.in_count, s.all_count, s.send_fp, s.send_ref, s.send_ans,  s.recv_fp,   s.recv_ans,
-                  s.new_count, s.all_new, s.rows_in,  s.rows_base, s.send_rows, s.recv_rows};
+                  s.new_count, s.all_new, s.rows_in,  s.rows_base, s.send_rows, s.recv_rows, s.queue, s.qcount};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -794,8 +798,9 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
                               2ull * G * x->rows_cap * (L.W + 2) * 4
                         : 0;
   const uint64_t sbytes = G > 1 ? 8ull << x->slog2 : 0;
+  const uint64_t qbytes = 8 * x->qcap;
   if (!x->front_cap) {
-    uint64_t used = tbytes + sbytes + pbytes + boxb;
+    uint64_t used = tbytes + sbytes + pbytes + boxb + qbytes;
     uint64_t rest = budget > used ? budget - used : 0;
     x->front_cap = std::max<uint64_t>(rest / rowb, 2048);
   }
@@ -825,6 +830,10 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
     s.h_all.assign((size_t)G * G, 0);
     HIPCHK(hipMalloc(&s.sent, sbytes));
     HIPCHK(hipMemsetAsync(s.sent, 0, sbytes, x->stream));
+  }
+  if (x->qcap) {
+    HIPCHK(hipMalloc(&s.queue, qbytes));
+    HIPCHK(hipMalloc(&s.qcount, 8));
   }
   HIPCHK(hipMemsetAsync(s.table, 0, tbytes, x->stream));
   HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
@@ -918,6 +927,20 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   // the sent cache is a dedup hint (one slot per fingerprint, overwritten on
   // a miss): a quarter of the set's slots
   x->slog2 = std::max(12, tl - 2);
+  // SYMMETRY on one shard: orbit keys in a kernel of their own (k_sym_keys),
+  // fed by a queue of (parent, instance) entries ~1/16 of the budget; the
+  // level runs in rounds of frontier states whose successors surely fit it
+  // (every instance enabled, a quarter lost to chunk holes)
+  if (L.sym && G == 1 && expand_compact_wpb(L) > 0 && launch_sym_keys_supported(L)) {
+    const char* q = getenv("RTLA_SYM_QUEUE");
+    if (!q || atoi(q) != 0) {
+      x->qcap = std::min<uint64_t>(per / 16 / 8, 1ull << 31);
+      const uint64_t holes = 256ull * 4096;  // a 256-entry chunk open per resident wave
+      const uint64_t usable = x->qcap > 2 * holes ? (x->qcap - holes) * 3 / 4 : 0;
+      x->qchunk = usable / (uint64_t)L.fam[F_COUNT] & ~63ull;
+      if (x->qchunk < 64) x->qcap = x->qchunk = 0;
+    }
+  }
   x->front_cap = cfg->frontier_cap;
   x->sh.resize(nlocal);
   for (int k = 0; k < nlocal; k++) {
@@ -947,11 +970,12 @@ extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
   snprintf(buf, cap,
            "{\"device\": \"%s\", \"arch\": \"%s\", \"cus\": %d, \"rank\": %d, \"world\": %d, \"shards\": %d, "
            "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu, "
-           "\"transport\": \"%s\", \"sent_cache_slots_log2\": %d, \"rebalanced_rows\": %llu}",
+           "\"transport\": \"%s\", \"sent_cache_slots_log2\": %d, \"rebalanced_rows\": %llu, "
+           "\"sym_key_queue\": %llu, \"sym_round_states\": %llu}",
            p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
            (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk,
            x->shm ? "shm" : x->comm ? (x->rccl_local ? "rccl-local" : "rccl") : "device", x->nshard > 1 ? x->slog2 : 0,
-           (unsigned long long)x->rebalanced);
+           (unsigned long long)x->rebalanced, (unsigned long long)x->qcap, (unsigned long long)x->qchunk);
   return RTLA_OK;
 }
 
@@ -1321,7 +1345,7 @@ static int move_answers(rtla_ctx* x) {
 // above it send their LAST rows, in shard order, to those below it (rows and
 // parent records, staged k_stage_rows -> exchange -> k_unpack_rows, in
 // sub-rounds of rows_cap).  Skipped while the largest excess is within
-// 2 % + 4096 rows of the split: a new state is stored by the shard that
+// 1 % + 64 rows of the split: a new state is stored by the shard that
 // generated it, so an even level stays about even, and after the first
 // levels (Init's successors all come from Init's shard) little moves.
 static int rebalance(rtla_ctx* x, std::vector<uint64_t>& n, const std::vector<uint64_t>& next_base,
@@ -1335,7 +1359,7 @@ static int rebalance(rtla_ctx* x, std::vector<uint64_t>& n, const std::vector<ui
     tgt[k] = total / G + ((uint64_t)k < total % G ? 1 : 0);
     if (n[k] > tgt[k]) worst = std::max(worst, n[k] - tgt[k]);
   }
-  if (worst <= 4096 + total / (50ull * G)) return RTLA_OK;
+  if (worst <= 64 + total / (100ull * G)) return RTLA_OK;
   auto local = [&](int id) -> Shard* {
     for (auto& s : x->sh)
       if (s.id == id) return &s;
@@ -1451,7 +1475,23 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
   }
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev0, x->stream));
-  if (G == 1) {
+  if (G == 1 && x->qcap && !(env_xflags() & XF_WAVE_KERNEL)) {
+    // SYMMETRY: per round, the level kernel evaluates and queues, k_sym_keys
+    // keys, probes and builds the new orbits' rows
+    Shard& s = x->sh[0];
+    ShardBox box{1, 0, (unsigned long long)x->qcap, 0, (unsigned long long*)s.qcount, nullptr,
+                 (unsigned long long*)s.queue};
+    for (uint64_t b = 0; b < s.n_cur; b += x->qchunk) {
+      const uint64_t e = std::min<uint64_t>(b + x->qchunk, s.n_cur);
+      HIPCHK(hipMemsetAsync(s.qcount, 0, 8, x->stream));
+      HIPCHK(launch_expand(L, cur_ring(x, s), b, e, s.cur_base, next_ring(x, s), s.parents, next_base[0],
+                           next_cap[0], s.table, x->tlog2, s.ctr, box, x->grid, x->stream,
+                           env_xflags() | XF_SYM_QUEUE, nullptr, nullptr));
+      HIPCHK(launch_sym_keys(L, cur_ring(x, s), s.cur_base, s.queue, s.qcount, x->qcap, next_ring(x, s), s.parents,
+                             next_base[0], next_cap[0], s.table, x->tlog2, s.ctr, x->stream));
+    }
+    HIPCHK(hipEventRecord(s.evm, x->stream));
+  } else if (G == 1) {
     Shard& s = x->sh[0];
     ShardBox box{1, 0, 0, 0, nullptr, nullptr, nullptr};
     uint64_t blocks = (s.n_cur + 3) / 4;

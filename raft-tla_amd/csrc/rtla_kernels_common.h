@@ -503,6 +503,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // queued by the evaluation pass and keyed 64 at a time (key_chunk)
   uint16_t* kring = ring + RING;
   int kpos = 0, kdone = 0;
+  // XF_SYM_QUEUE: this wave's open chunk of the HBM key queue (wave-uniform)
+  unsigned long long qb = ~0ull;
+  int qu = OBOX_CHUNK;
   uint32_t* cstage = reinterpret_cast<uint32_t*>(kring + (SYM ? RING : 0));  // CSTAGE child rows
   if (MULTI) {
     if (lane < SHARD_MAX) {
@@ -873,8 +876,28 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     }
     if constexpr (KSPLIT) {
       const unsigned long long km = __ballot(kq);
-      if (kq) kring[(kpos + __popcll(km & lanes_below)) & (RING - 1)] = (uint16_t)(sl << 8 | inst);
-      kpos += __popcll(km);
+      if (xflags & XF_SYM_QUEUE) {  // to the HBM queue, for k_sym_keys
+        if (km) {
+          const int cnt = __popcll(km);
+          if (qu + cnt > OBOX_CHUNK) {  // close the open chunk (holes = ~0), reserve the next
+            if (qb != ~0ull)
+              for (unsigned long long j = qb + qu + lane; j < min(qb + OBOX_CHUNK, box.cap); j += 64) box.send_ref[j] = ~0ull;
+            unsigned long long nb = 0;
+            if (lane == 0) nb = atomicAdd(box.out_count, (unsigned long long)OBOX_CHUNK);
+            qb = shfl0_u64(nb);
+            qu = 0;
+          }
+          if (kq) {
+            const unsigned long long slot = qb + qu + __popcll(km & lanes_below);
+            if (slot < box.cap) box.send_ref[slot] = (s0 + sl) << 16 | (unsigned long long)inst;
+            else set_flag(ctr, FLAG_OUTBOX_FULL);
+          }
+          qu += cnt;
+        }
+      } else {
+        if (kq) kring[(kpos + __popcll(km & lanes_below)) & (RING - 1)] = (uint16_t)(sl << 8 | inst);
+        kpos += __popcll(km);
+      }
     }
     if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
       const int code = en ? cover_code(L, inst, d.sub) : -1;
@@ -1085,6 +1108,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
     }
   }
+  if (KSPLIT && (xflags & XF_SYM_QUEUE) && qb != ~0ull)
+    for (unsigned long long j = qb + qu + lane; j < min(qb + OBOX_CHUNK, box.cap); j += 64) box.send_ref[j] = ~0ull;
   for (int off = 32; off > 0; off >>= 1) {
     my_gen += __shfl_down(my_gen, off);
     my_probe += __shfl_down(my_probe, off);

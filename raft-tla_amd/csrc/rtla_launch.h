@@ -65,6 +65,12 @@ hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* count
                               uint64_t next_cap, DevCounters* ctr, uint64_t max_count, hipStream_t st);
 hipError_t launch_stage_rows(int W, const Ring& next, const uint64_t* parents, uint64_t next_base, uint64_t first,
                              uint64_t n, uint32_t* rows, hipStream_t st);
+// SYMMETRY, one shard: orbit keys + probes + new rows of the queued successors (rtla_ksymkeys.hip).
+bool launch_sym_keys_supported(const Layout& L);
+hipError_t launch_sym_keys(const Layout& L, const Ring& cur, uint64_t cur_base, const uint64_t* queue,
+                           const uint64_t* qcount, uint64_t qcap, const Ring& next, uint64_t* parents,
+                           uint64_t next_base, uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr,
+                           hipStream_t st);
 hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
                               int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st);
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,

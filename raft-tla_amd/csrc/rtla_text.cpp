@@ -26,7 +26,12 @@ namespace {
 struct Out {
   char* p;
   size_t n = 0;
-  void s(const char* t) {
+  template <size_t K>
+  void s(const char (&t)[K]) {  // a literal: its length is known at compile time
+    memcpy(p + n, t, K - 1);
+    n += K - 1;
+  }
+  void str(const char* t) {  // a run-time string
     const size_t k = strlen(t);
     memcpy(p + n, t, k);
     n += k;
@@ -95,7 +100,7 @@ void text_msg(Out& o, uint64_t k, const int* pi = nullptr) {
   static const char* TN[4] = {"RequestVoteRequest", "RequestVoteResponse", "AppendEntriesRequest",
                               "AppendEntriesResponse"};
   o.s("[mtype |-> \"");
-  o.s(TN[m_type(k)]);
+  o.str(TN[m_type(k)]);
   o.s("\", mterm |-> ");
   o.u(m_term(k));
   o.s(", ");
@@ -109,7 +114,7 @@ void text_msg(Out& o, uint64_t k, const int* pi = nullptr) {
       break;
     case RVRESP:
       o.s("mvoteGranted |-> ");
-      o.s(BOOL(m_f(k, 12, 1)));
+      o.str(BOOL(m_f(k, 12, 1)));
       o.s(", mlog |-> ");
       text_log(o, m_f(k, 16, 28));
       o.s(", ");
@@ -139,7 +144,7 @@ void text_msg(Out& o, uint64_t k, const int* pi = nullptr) {
     }
     case AERESP:
       o.s("msuccess |-> ");
-      o.s(BOOL(m_f(k, 12, 1)));
+      o.str(BOOL(m_f(k, 12, 1)));
       o.s(", mmatchIndex |-> ");
       o.u(m_f(k, 13, 3));
       o.s(", ");
@@ -166,7 +171,7 @@ struct Items {
   }
   // std::string ordering: bytewise, a proper prefix first
   void emit(Out& o, const char* open, const char* sep, const char* close, const char* empty) {
-    if (!n) return o.s(empty);
+    if (!n) return o.str(empty);
     uint16_t ord[KMAX + EMAX + 32 * 32 + 1];
     for (int k = 0; k < n; k++) ord[k] = (uint16_t)k;
     const char* base = scratch.p;
@@ -175,13 +180,13 @@ struct Items {
       const int r = memcmp(base + off[a], base + off[b], std::min(la, lb));
       return r < 0 || (r == 0 && la < lb);
     });
-    o.s(open);
+    o.str(open);
     for (int k = 0; k < n; k++) {
-      if (k) o.s(sep);
+      if (k) o.str(sep);
       memcpy(o.p + o.n, base + off[ord[k]], len[ord[k]]);
       o.n += len[ord[k]];
     }
-    o.s(close);
+    o.str(close);
     n = 0;
     scratch.n = 0;
   }
@@ -288,7 +293,7 @@ void line_server(Out& o, const Dec& d, int k, const int* pi, const int* sg) {
   static const char* RN[4] = {"\"Follower\"", "\"Candidate\"", "\"Leader\"", "\"?\""};
   const int N = d.N;
   o.s("/\\ ");
-  o.s(NAME[k]);
+  o.str(NAME[k]);
   o.s(" = (");
   for (int p = 0; p < N; p++) {
     const uint32_t* r = d.rec[sg ? sg[p] : p];
@@ -297,7 +302,7 @@ void line_server(Out& o, const Dec& d, int k, const int* pi, const int* sg) {
     o.s(" :> ");
     switch (k) {
       case 0: o.u(s_term(r[0])); break;
-      case 1: o.s(RN[s_role(r[0])]); break;
+      case 1: o.str(RN[s_role(r[0])]); break;
       case 2:
         if (s_voted(r[0]) == NIL) o.s("\"Nil\"");
         else o.srv(pi ? (uint32_t)pi[s_voted(r[0])] : s_voted(r[0]));
@@ -399,7 +404,7 @@ size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, ch
   if (work.size() < 2 * cap) work.resize(2 * cap);
   char* bufs[2] = {work.data(), work.data() + cap};
   int bi = -1;
-  size_t bn = 0;
+  size_t bn = 0, bmsg = 0;  // the best's length and the offset of its messages line ("\n" before it)
   Items it;
   it.scratch.p = scratch;
   for (;;) {
@@ -407,6 +412,7 @@ size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, ch
     const int ci = bi < 0 ? 0 : bi ^ 1;
     Out o{bufs[ci]};
     bool below = bi < 0, above = false;
+    size_t msg_off = 0;
     auto cmp_line = [&](size_t from) {  // the line just written: below / above / equal to best's bytes
       if (below) return;
       const int r = memcmp(o.p + from, bufs[bi] + from, o.n - from);
@@ -415,6 +421,7 @@ size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, ch
     };
     for (int k = 2; k < SRV_LINES + 3 && !above; k++) {
       const size_t from = o.n;
+      if (k == SRV_LINES) msg_off = from;
       o.c('\n');
       if (k < SRV_LINES) line_server(o, d, k, pi, sg);
       else if (k == SRV_LINES) line_messages(o, it, d, pi);
@@ -425,6 +432,7 @@ size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, ch
     if (below) {
       bi = ci;
       bn = o.n;
+      bmsg = msg_off;
       for (int p = 0; p < N; p++) best_sg[p] = sg[p];
     }
     // next ordering: an odometer over the tie groups' permutations
@@ -432,9 +440,20 @@ size_t state_orbit_text_into(const Layout& L, const uint32_t* row, char* buf, ch
     while (g >= 0 && !std::next_permutation(sg + gb[g], sg + gb[g + 1])) g--;
     if (g < 0) break;
   }
-  (void)bn;
+  // the best image's text in TLC order, from its rotated text: messages,
+  // elections, allLogs, then the two lines every candidate shares, then the
+  // other eight per-server lines
   for (int p = 0; p < N; p++) pi[best_sg[p]] = p;
-  return image_text(L, row, d, pi, best_sg, buf, scratch);
+  Out o{buf};
+  memcpy(o.p, bufs[bi] + bmsg + 1, bn - bmsg - 1);
+  o.n = bn - bmsg - 1;
+  for (int k = 0; k < 2; k++) {
+    o.c('\n');
+    line_server(o, d, k, pi, best_sg);
+  }
+  memcpy(o.p + o.n, bufs[bi], bmsg);
+  o.n += bmsg;
+  return o.n;
 }
 
 std::string state_text(const Layout& L, const uint32_t* row) {
