@@ -87,8 +87,6 @@ struct Shard {
   uint32_t* send_ans = nullptr;    // [G][cap]  owners' answers to our records
   uint64_t* recv_fp = nullptr;     // [G][cap][2]
   uint32_t* recv_ans = nullptr;    // [G][cap]  our answers to the senders
-  uint64_t* new_count = nullptr;   // [G] device: new fingerprints we own, per source
-  uint64_t* all_new = nullptr;     // [G][G] device (unused since the two-phase exchange)
   uint64_t* rows_in = nullptr;     // [G] device: rows received per source (re-balancing sub-round)
   uint64_t* rows_base = nullptr;   // [G] device: next-frontier slot of each source's first row
   uint32_t* send_rows = nullptr;   // [G][rows_cap][W + 2]  re-balancing staging
@@ -764,7 +762,7 @@ extern "C" int rtla_comm_id(void* out128) {
 static void free_shard(Shard& s) {
   void* ptrs[] = {s.table,    s.sent,     s.parents,  s.arena,    s.ctr,       s.dflags,    s.out_count,
                   s.in_count, s.all_count, s.send_fp, s.send_ref, s.send_ans,  s.recv_fp,   s.recv_ans,
-                  s.new_count, s.all_new, s.rows_in,  s.rows_base, s.send_rows, s.recv_rows, s.queue, s.qcount};
+                  s.rows_in,  s.rows_base, s.send_rows, s.recv_rows, s.queue, s.qcount};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -819,8 +817,6 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
     HIPCHK(hipMalloc(&s.send_ans, 4 * G * x->box_cap));
     HIPCHK(hipMalloc(&s.recv_fp, 16 * G * x->box_cap));
     HIPCHK(hipMalloc(&s.recv_ans, 4 * G * x->box_cap));
-    HIPCHK(hipMalloc(&s.new_count, 8 * G));
-    HIPCHK(hipMalloc(&s.all_new, 8 * G * G));
     HIPCHK(hipMalloc(&s.rows_in, 8 * G));
     HIPCHK(hipMalloc(&s.rows_base, 8 * G));
     HIPCHK(hipMalloc(&s.send_rows, 4ull * G * x->rows_cap * (L.W + 2)));
@@ -932,8 +928,8 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   // level runs in rounds of frontier states whose successors surely fit it
   // (every instance enabled, a quarter lost to chunk holes)
   if (L.sym && G == 1 && expand_compact_wpb(L) > 0 && launch_sym_keys_supported(L)) {
-    const char* q = getenv("RTLA_SYM_QUEUE");
-    if (!q || atoi(q) != 0) {
+    const char* q = getenv("RTLA_SYM_QUEUE");  // opt-in: measured slower than keys in the level kernel
+    if (q && atoi(q) != 0) {
       x->qcap = std::min<uint64_t>(per / 16 / 8, 1ull << 31);
       const uint64_t holes = 256ull * 4096;  // a 256-entry chunk open per resident wave
       const uint64_t usable = x->qcap > 2 * holes ? (x->qcap - holes) * 3 / 4 : 0;
@@ -1520,11 +1516,10 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
       rc = move_fps(x);
       if (rc) return rc;
       for (auto& s : x->sh) {
-        HIPCHK(hipMemsetAsync(s.new_count, 0, 8 * G, x->stream));
         uint64_t mx_in = 0;
         for (uint64_t v : s.h_in) mx_in = std::max(mx_in, v);
-        HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_ans, s.new_count,
-                                    s.ctr, mx_in, x->stream));
+        HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_ans, s.ctr, mx_in,
+                                    x->stream));
       }
       rc = move_answers(x);
       if (rc) return rc;

@@ -13,43 +13,44 @@
 using namespace rtla;
 
 // Owner side of the exchange: insert the fingerprints other shards sent and
-// answer each record with 0 (seen) or 1 + its dense rank among the new
-// fingerprints from that source (the sender uses the rank as the row slot it
-// ships the materialised state into).  Region p holds counts[p] records.
+// answer each record with 1 (new: the sender builds the state) or 0 (seen).
+// Region p (grid.y) holds counts[p] records.  Each thread takes IR records a
+// stride apart and issues their home-slot loads together (IR random reads
+// in flight per lane); no per-wave atomics (the two-phase exchange needs no
+// dense ranks).
+constexpr int IR = 4;
 __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
                                 const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
-                                unsigned long long* table, int tlog2, uint32_t* __restrict__ ans,
-                                unsigned long long* __restrict__ new_count, DevCounters* ctr) {
-  // grid.y = source shard p; lanes of a wave share p, so one atomic per wave
-  // hands out the dense ranks of its new fingerprints
+                                unsigned long long* table, int tlog2, uint32_t* __restrict__ ans, DevCounters* ctr) {
   const unsigned long long p = blockIdx.y;
   const unsigned long long n = counts[p];
   const int lane = threadIdx.x & 63;
   unsigned probes = 0;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long k0 = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); k0 < n;
-       k0 += stride) {
-    const unsigned long long k = k0 + lane;
-    int r = 0;
-    if (k < n) {
-      const unsigned long long i = p * cap + k;
-      const FP f{recv_fp[2 * i], recv_fp[2 * i + 1]};
-      if (f.a | f.b) {  // 0:0 = a hole in the sender's outbox chunk
-        // load first (the owner may know the state already: a plain load is
-        // cheaper than an atomic at the memory side), CAS only an empty slot
-        const unsigned long long key = f.b | 1ull, idx = f.a >> (64 - tlog2);
-        const unsigned long long seen = __hip_atomic_load(&table[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        r = fpset_resolve_loaded(table, tlog2, key, idx, seen, ctr) ? 1 : 0;
+  for (unsigned long long k0 = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k0 < n; k0 += IR * stride) {
+    FP f[IR];
+    unsigned long long seen[IR];
+#pragma unroll
+    for (int u = 0; u < IR; u++) {
+      const unsigned long long k = k0 + u * stride;
+      f[u] = k < n ? FP{recv_fp[2 * (p * cap + k)], recv_fp[2 * (p * cap + k) + 1]} : FP{0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < IR; u++)  // load first (the owner may know the state: a load is cheaper than an atomic)
+      seen[u] = (f[u].a | f[u].b) ? __hip_atomic_load(&table[f[u].a >> (64 - tlog2)], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0ull;
+#pragma unroll
+    for (int u = 0; u < IR; u++) {
+      const unsigned long long k = k0 + u * stride;
+      if (k >= n) continue;
+      uint32_t r = 0;
+      if (f[u].a | f[u].b) {  // 0:0 = a hole in the sender's outbox chunk
+        r = fpset_resolve_loaded(table, tlog2, f[u].b | 1ull, f[u].a >> (64 - tlog2), seen[u], ctr) ? 1u : 0u;
         probes++;
       }
+      ans[p * cap + k] = r;
     }
-    const unsigned long long m = __ballot(r == 1);
-    unsigned long long b = 0;
-    if (m) {
-      if (lane == 0) b = atomicAdd(&new_count[p], (unsigned long long)__popcll(m));
-      b = shfl0_u64(b);
-    }
-    if (k < n) ans[p * cap + k] = r == 1 ? (uint32_t)(b + __popcll(m & ((1ull << lane) - 1ull))) + 1u : 0u;
   }
   for (int off = 32; off > 0; off >>= 1) probes += __shfl_down(probes, off);
   if (lane == 0 && probes) atomicAdd(&ctr->probes, (unsigned long long)probes);
@@ -240,13 +241,12 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
 }
 
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
-                                uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
-                                uint64_t max_count, hipStream_t st) {
+                                uint64_t* table, int tlog2, uint32_t* ans, DevCounters* ctr, uint64_t max_count,
+                                hipStream_t st) {
   if (!max_count) return hipSuccess;
-  hipLaunchKernelGGL(k_insert_remote, dim3(grid_x(max_count, 256), nshard), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_insert_remote, dim3(grid_x((max_count + IR - 1) / IR, 256), nshard), dim3(256), 0, st,
                      (const unsigned long long*)recv_fp, (const unsigned long long*)counts, nshard,
-                     (unsigned long long)cap, (unsigned long long*)table, tlog2, ans, (unsigned long long*)new_count,
-                     ctr);
+                     (unsigned long long)cap, (unsigned long long*)table, tlog2, ans, ctr);
   return hipGetLastError();
 }
 

@@ -36,57 +36,69 @@ k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
   __syncthreads();
   const unsigned long long p = blockIdx.y;  // owner shard
   const unsigned long long n = counts[p];
-  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; k0 < n;
-       k0 += (unsigned long long)gridDim.x * wpb * 64ull) {
-    const unsigned long long k = k0 + lane;
-    const unsigned long long i = p * cap + k;
-    const bool win = k < n && ans[i] != 0u;
-    const unsigned long long m = __ballot(win);
-    if (!m) continue;
-    const int nw = __popcll(m);
-    // lane r takes the r-th winner's record
-    int src_lane = 0;
-    {
-      unsigned long long mm = m;
-      for (int r = 0; r < nw; r++) {
-        const int l = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        if (lane == r) src_lane = l;
-      }
+  constexpr int SUB = 4;  // 64-record pieces per wave block: one next-level reservation for all their winners
+  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * (64ull * SUB); k0 < n;
+       k0 += (unsigned long long)gridDim.x * wpb * 64ull * SUB) {
+    unsigned long long mk[SUB];
+    int tot = 0;
+#pragma unroll
+    for (int u = 0; u < SUB; u++) {
+      const unsigned long long k = k0 + u * 64ull + lane;
+      mk[u] = __ballot(k < n && ans[p * cap + k] != 0u);
+      tot += __popcll(mk[u]);
     }
-    const unsigned long long ref = shfl_u64(win ? send_ref[i] : 0ull, src_lane);
-    const bool act = lane < nw;
-    const unsigned long long s = ref >> 16;  // parent: state s of the current level
-    const int inst = (int)(ref & 0xffffull);
-    gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
-    wave_sync();
-    uint32_t* prow = lrows + lane * W;
+    if (!tot) continue;
     unsigned long long obase = 0;
-    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)nw);
+    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)tot);
     obase = shfl0_u64(obase);
-    if (act) {
-      const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
-      DeltaT<NS> d;
-      compute_delta<NS>(L, prow, inst, d);
-      const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
-      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-      if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-          atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-        ctr->viol_parent = cur_base + s;
-        ctr->viol_inst = inst;
-        ctr->viol_in_model = 1;
-        ctr->viol_child = obase + lane < next_cap ? next_base + obase + lane : ~0ull;
+    if (obase + tot > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    for (int u = 0; u < SUB; u++) {
+      const unsigned long long m = mk[u];
+      if (!m) continue;
+      const int nw = __popcll(m);
+      // lane r takes the r-th winner's record
+      int src_lane = 0;
+      {
+        unsigned long long mm = m;
+        for (int r = 0; r < nw; r++) {
+          const int l = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          if (lane == r) src_lane = l;
+        }
       }
-      atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
-      materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
+      const unsigned long long i = p * cap + k0 + u * 64ull + lane;
+      const unsigned long long ref = shfl_u64((m >> lane & 1ull) ? send_ref[i] : 0ull, src_lane);
+      const bool act = lane < nw;
+      const unsigned long long s = ref >> 16;  // parent: state s of the current level
+      const int inst = (int)(ref & 0xffffull);
+      gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
+      wave_sync();
+      uint32_t* prow = lrows + lane * W;
+      if (act) {
+        const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
+        DeltaT<NS> d;
+        compute_delta<NS>(L, prow, inst, d);
+        const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
+        const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+        if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+          ctr->viol_parent = cur_base + s;
+          ctr->viol_inst = inst;
+          ctr->viol_in_model = 1;
+          ctr->viol_child = obase + lane < next_cap ? next_base + obase + lane : ~0ull;
+        }
+        atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
+        materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
+      }
+      wave_sync();
+      const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nw, next_cap - obase);
+      store_rows_ring(next, obase, nrows, W, lrows, lane);
+      if (lane < nrows)
+        parents[next_base + obase + lane] =
+            (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
+      obase += nw;
+      wave_sync();
     }
-    wave_sync();
-    if (obase + nw > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
-    const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nw, next_cap - obase);
-    store_rows_ring(next, obase, nrows, W, lrows, lane);
-    if (lane < nrows)
-      parents[next_base + obase + lane] = (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
-    wave_sync();
   }
   __syncthreads();
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
@@ -163,7 +175,7 @@ static hipError_t build_winners(const Layout& L, const Ring& cur, uint64_t cur_b
                                 uint64_t max_count, hipStream_t st) {
   const int wpb = std::max(1, expand_lane_wpb(L));
   const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-  hipLaunchKernelGGL((k_build_winners<NS, LC>), dim3(grid_x(max_count, 64 * wpb), nshard), dim3(64 * wpb), lds, st,
+  hipLaunchKernelGGL((k_build_winners<NS, LC>), dim3(grid_x(max_count, 256 * wpb), nshard), dim3(64 * wpb), lds, st,
                      L, cur, (unsigned long long)cur_base, me, (const unsigned long long*)send_ref, ans,
                      (const unsigned long long*)counts, nshard, (unsigned long long)cap, next,
                      (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap, ctr);

@@ -80,8 +80,17 @@ k_sym_keys(Layout Lrt, Ring cur, unsigned long long cur_base, const unsigned lon
     const bool valid = e != ~0ull;  // (~0: a hole of the level kernel's queue chunks)
     const unsigned long long s = valid ? e >> 16 : 0ull;  // parent: state s of the current level
     const int inst = valid ? (int)(e & 0xffffull) : 0;
-    // 1. parents -> LDS, each lane's turned into its successor in place
-    gather_rows_lds(rows, W, KQ, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
+    // 1. parents -> LDS by LDS-DMA (one global_load_lds_dword per row and
+    // 64 words, every row in flight at once), then each lane turns its row
+    // into its successor in place
+    for (int r2 = 0; r2 < KQ; r2++) {
+      const uint32_t* src = ring_row(cur, readlane_u64(s, r2), W);
+      for (int c0 = 0; c0 < W; c0 += 64)
+        if (c0 + lane < W)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c0 + lane),
+                                           (__attribute__((address_space(3))) void*)(rows + r2 * W + c0), 4, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     uint32_t* const srow = rows + lane * W;
     int sub = 0;

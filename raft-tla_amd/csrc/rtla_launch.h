@@ -54,8 +54,8 @@ hipError_t launch_wave_expand(const Layout& L, const Ring& cur, uint64_t s_begin
                               uint64_t* table, int tlog2, DevCounters* ctr, const ShardBox& box, int grid,
                               hipStream_t st);
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,
-                                uint64_t* table, int tlog2, uint32_t* ans, uint64_t* new_count, DevCounters* ctr,
-                                uint64_t max_count, hipStream_t st);
+                                uint64_t* table, int tlog2, uint32_t* ans, DevCounters* ctr, uint64_t max_count,
+                                hipStream_t st);
 hipError_t launch_build_winners(const Layout& L, const Ring& cur, uint64_t cur_base, int me, const uint64_t* send_ref,
                                 const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap,
                                 const Ring& next, uint64_t* parents, uint64_t next_base, uint64_t next_cap,

@@ -527,6 +527,31 @@ def test_symmetry_virtual_shards_match_golden(name, shards):
     assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
 
 
+@pytest.mark.parametrize("name", ["n3_v1_t2_l1_m1_sym", "n3_v1_t3_l1_m1_ntl_sym", "n4_v1_t2_l1_m1_sym_prefix"])
+def test_symmetry_key_kernel_matches_golden(monkeypatch, name):
+    """The separate SYMMETRY key kernel (RTLA_SYM_QUEUE=1: the level kernel
+    queues, k_sym_keys materialises, ranks, spreads the images over the
+    lanes, probes and builds): golden per-level orbit counts and orbit-text
+    digests, and the counterexample of the NoTwoLeaders model."""
+    monkeypatch.setenv("RTLA_SYM_QUEUE", "1")
+    g = GOLD[name]
+    kw = small_kw(g) if not g.get("prefix") else dict(fpset_log2=26)
+    want, digest = level_digests(g)
+    with rtla.Checker(cfg_of(g, **kw)) as ck:
+        assert json.loads(ck.device_info())["sym_key_queue"] > 0
+        st = ck.init()
+        got = []
+        while True:
+            got.append("%016x" % digest(ck))
+            if st != rtla.OK or len(ck.levels) >= len(g["levels"]):
+                break
+            st = ck.step()
+        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
+        assert got == want[:len(got)] and len(got) >= len(want) - 1
+        if g.get("violated"):
+            assert st == rtla.VIOLATION and len(ck.trace()) == g["trace_len"]
+
+
 @pytest.mark.parametrize("shards", [1, 2])
 def test_symmetry_counterexample_trace(shards):
     """Same shortest depth as without symmetry; the trace is made of the
