@@ -264,6 +264,25 @@ __device__ __forceinline__ FP successor_orbit_key(const Layout& L, P prow, const
   });
 }
 
+// The orbit key in steps of one image (key_chunk's continuations): images
+// [k, k + 1) of the successor parent + d -- or [k, |C(s)|) when `all` --
+// folded into best (the least image fingerprint so far).  Returns the next
+// image's index, or -1 once best is the least image (the key is then
+// orbit_key_finish(best) + fp(allLogs'), as sym_key's).
+template <int NS, class P>
+__device__ __forceinline__ int successor_orbit_step(const Layout& L, P prow, const DeltaT<NS>& d, int k, bool all,
+                                                    FP& best) {
+  return with_successor<NS>(L, prow, d, [&](auto rec_of, int nmsg, auto slot_of, int nelec, auto elec_of) {
+    const SymRank r = sym_rank<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of);
+    const int k1 = all ? r.ncomb : min(k + 1, r.ncomb);
+    for (int j = k; j < k1; j++) {
+      const FP f = sym_image_fp<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of, r, j);
+      if (fp_less(f, best)) best = f;
+    }
+    return k1 < r.ncomb ? k1 : -1;
+  });
+}
+
 // Load the parent row into LDS and derive the per-parent data every lane
 // needs.  Returns the parent fingerprint with allLogs' already applied.
 template <int NS>
@@ -343,7 +362,8 @@ constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a 
 // per-state fingerprint with allLogs' applied (GROUP FPs) | SYMMETRY: the
 // fingerprint of each state's allLogs' (GROUP FPs) | per-owner (base, used)
 // of the open outbox chunk | pending new states (NEWCAP u16 entries) |
-// GROUP rows | allLogs' words of each state | pair ring | SYMMETRY: key ring.
+// GROUP rows | allLogs' words of each state | pair ring | SYMMETRY: key ring,
+// key continuations (64 least-image-so-far FPs, 64 entries).
 // (The outbox state exists only in the MULTI kernels: one shard's tile then
 // stays small enough for 12 one-wave blocks per CU on configs[1]'s 372-byte rows.)
 // RTLA_CHILD_STAGE > 0: child rows are built in an LDS stage of that many
@@ -358,7 +378,7 @@ constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a 
 constexpr int CSTAGE = RTLA_CHILD_STAGE;
 __host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym, bool multi) {
   return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW +
-          RING / 2 * (sym ? 2 : 1) + CSTAGE * W + 3) & ~3;
+          RING / 2 * (sym ? 2 : 1) + (sym ? 5 * 64 : 0) + CSTAGE * W + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -429,7 +449,8 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #define RTLA_COMPACT_WAVES_PER_EU 3  // 168 VGPRs (3 waves/SIMD); spills per instantiation: profiles/r04_*/resource_usage.txt
 #endif
 #ifndef RTLA_SYM_WAVES_PER_EU
-#define RTLA_SYM_WAVES_PER_EU 3      // SYMMETRY: 168 VGPRs with spills beats 256 without (configs[3]: 356 vs 406 ms)
+#define RTLA_SYM_WAVES_PER_EU 4      // SYMMETRY, the key pass a call of its own (key_one): 128 VGPRs (configs[3]:
+                                     // 311.5 ms, 16-state groups) beat 168 (343 ms) and 102 (414 ms)
 #endif
 #ifndef RTLA_MULTI_ASYNC
 #define RTLA_MULTI_ASYNC 1  // multi-shard kernels pipeline their CAS too
@@ -445,6 +466,39 @@ __device__ __forceinline__ const Layout& pick_layout(const Layout& rt) {
   if constexpr (LC.N == 0) return rt;
   else return LC;
 }
+
+namespace {
+// One key_chunk lane as a function of its own: the successor's Delta, then
+// successor_orbit_step from image k with the least image so far best0.
+// next >= 0: f is the least image so far and image `next` is due; next ==
+// -1: f is the orbit key; next == -2: the instance is not enabled.  NOT
+// inlined, so that its registers are allocated apart from the level
+// kernel's: inlined, the continuation bookkeeping spilled the kernel to 712
+// VGPRs (750 ms per configs[3] step); as a call, 343 ms against 355 ms for
+// the inlined all-images key pass (profiles/r04_v4).
+struct KeyStep {
+  FP f;
+  int next;
+};
+template <int NS, Layout LC>
+__device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow, int inst, int k, bool all, FP best0,
+                                        FP afp) {
+  const Layout& L = pick_layout<LC>(Lrt);
+  DeltaT<NS> d;
+  d.enabled = 0;
+  compute_delta<NS>(L, prow, inst, d);
+  KeyStep r{FP{0, 0}, -1};
+  if (!d.enabled) {
+    r.next = -2;
+    return r;
+  }
+  FP best = best0;
+  r.next = successor_orbit_step<NS>(L, prow, d, k, all, best);
+  r.f = r.next < 0 ? fp_add(orbit_key_finish(best), afp) : best;
+  return r;
+}
+
+}  // namespace
 
 // RTLA_STAMPS (diagnostic builds only): per-wave cycle counts of the level
 // kernel's phases from s_memtime (each stamp waits for the wave's LDS
@@ -506,7 +560,14 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // XF_SYM_QUEUE: this wave's open chunk of the HBM key queue (wave-uniform)
   unsigned long long qb = ~0ull;
   int qu = OBOX_CHUNK;
-  uint32_t* cstage = reinterpret_cast<uint32_t*>(kring + (SYM ? RING : 0));  // CSTAGE child rows
+  // SYMMETRY: successors whose orbit key needs more images than key_chunk
+  // computes per pass (one): entry (state lane << 8 | instance | next image
+  // << 16) and the least image fingerprint so far; taken first by the next
+  // key chunk (ccount of them, uniform)
+  FP* cbest = reinterpret_cast<FP*>(kring + (SYM ? RING : 0));
+  uint32_t* cent = reinterpret_cast<uint32_t*>(cbest + (SYM ? 64 : 0));
+  int ccount = 0;
+  uint32_t* cstage = cent + (SYM ? 64 : 0);  // CSTAGE child rows
   if (MULTI) {
     if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
@@ -922,32 +983,58 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       ctr->viol_child = ~0ull;
     }
   };
-  // SYMMETRY: the orbit keys of kring[kd, kd + kc), one per lane: the full
-  // Delta (the probe pass only folded it into a hash), then
-  // successor_orbit_key; the key goes through the probe pipeline.  Kept
-  // apart from the evaluation pass so that neither holds the other's
-  // registers.  (Spreading a chunk's permutation images over the wave --
-  // reachable configs[3] states compare 2.2 images on average but the
-  // slowest of 64 lanes 7.5 -- was built and measured: 2.1-2.4x slower, the
-  // recomputed Deltas and the LDS min-reduction cost more than the
-  // divergence they remove.)
-  auto key_chunk = [&](int kd, int kc) {
-    const bool active = lane < kc;
-    const int e = active ? kring[(kd + lane) & (RING - 1)] : 0;
+  // SYMMETRY: orbit keys, one successor per lane: the ccount continuations
+  // first, then kring[kd, kd + kc) -- the full Delta (the probe pass only
+  // folded it into a hash), the signatures, and ONE permutation image per
+  // pass (`last`: all that are left); a successor with more images left
+  // continues in the next key chunk, the others' keys go through the probe
+  // pipeline.  Images computed one per pass keep the wave from waiting for
+  // its slowest lane: configs[3]'s successors compare 1.15 images on average
+  // but the slowest lane of a 64-successor chunk 2.31 (level-15 successors,
+  // tools/symstat.cpp; profiles/r04_v4/symstat.txt).
+  // Kept apart from the evaluation pass so that neither holds the other's
+  // registers.  (Spreading one successor's images over several lanes was
+  // built and measured: 2.1-2.4x slower, the recomputed Deltas and the LDS
+  // min-reduction cost more than the divergence they remove.)
+  auto key_chunk = [&](int kd, int kc, bool last) {
+    const int cn = ccount;
+    const bool cont = lane < cn;
+    const bool active = lane < cn + kc;
+    int e = 0, k = 0;
+    if (cont) {
+      const uint32_t ce = cent[lane];
+      e = (int)(ce & 0xffffu);
+      k = (int)(ce >> 16);
+    } else if (active) {
+      e = kring[(kd + lane - cn) & (RING - 1)];
+    }
     const int sl = e >> 8, inst = e & 255;
     const uint32_t* prow = rows + sl * W;
-    DeltaT<NS> d;
-    d.enabled = 0;
-    if (active) compute_delta<NS>(L, prow, inst, d);  // (generic: the per-family switch costs spills here)
     nprobe = false;
     ninfo_new = (uint32_t)sl << 16 | (uint32_t)inst;
-    if (active && d.enabled) {
-      const FP key = successor_orbit_key<NS>(L, prow, d, afpl[sl]);
-      nprobe = !(xflags & XF_NO_PROBE);
-      ncf = key;
-      nowner = MULTI ? fp_owner(key, box.nshard) : me;
-      nidx = key.a >> (64 - ((MULTI && nowner != me) ? box.slog2 : tlog2));
+    int next = -1;
+    FP best{~0ull, ~0ull};
+    if (active) {
+      const KeyStep ks = key_one<NS, LC>(Lrt, prow, inst, k, last, cont ? cbest[lane] : FP{~0ull, ~0ull}, afpl[sl]);
+      next = ks.next < 0 ? -1 : ks.next;
+      best = ks.f;
+      if (ks.next == -1) {
+        const FP key = ks.f;
+        nprobe = !(xflags & XF_NO_PROBE);
+        ncf = key;
+        nowner = MULTI ? fp_owner(key, box.nshard) : me;
+        nidx = key.a >> (64 - ((MULTI && nowner != me) ? box.slog2 : tlog2));
+      }
     }
+    const unsigned long long cm = __ballot(next >= 0);
+    wave_sync();  // (every lane has read its continuation)
+    if (next >= 0) {
+      const int c = __popcll(cm & lanes_below);
+      cent[c] = (uint32_t)e | (uint32_t)next << 16;
+      cbest[c] = best;
+    }
+    ccount = __popcll(cm);
+    wave_sync();
   };
   auto issue_probe = [&]() {
     asm volatile("" ::: "memory");
@@ -1051,16 +1138,25 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         STAMP(1);  // pair ring
         eval_chunk(done, cnt);
         STAMP(2);  // successor deltas, fingerprints, coverage, out-of-model invariants
-        if (!KSPLIT || (xflags & XF_ALL_SUCCESSORS) || kpos - kdone >= 64) {
-          if (KSPLIT && kpos - kdone >= 64) {  // 64 orbit keys are queued: key them (they feed the probe pipeline)
-            key_chunk(kdone, 64);
-            kdone += 64;
-            STAMP(7);  // SYMMETRY: orbit keys
-          }
+        if (!KSPLIT || (xflags & XF_ALL_SUCCESSORS)) {
           resolve();  // the previous chunk's probes, after this chunk's arithmetic
           STAMP(3);
           issue_probe();
           STAMP(4);  // probe issue
+        } else {
+          // 64 orbit keys to compute (continuations first): key them (they
+          // feed the probe pipeline) until fewer than 64 are queued (the key
+          // ring holds RING = 128; an evaluation chunk adds at most 64)
+          while (kpos - kdone + ccount >= 64) {
+            const int kc = min(kpos - kdone, 64 - ccount);
+            key_chunk(kdone, kc, kc == 0);
+            kdone += kc;
+            STAMP(7);  // SYMMETRY: orbit keys
+            resolve();
+            STAMP(3);
+            issue_probe();
+            STAMP(4);  // probe issue
+          }
         }
         if (tail - head > NEWFLUSH) {  // rare (early levels): drain the probes, build the rows so far
           drain();
@@ -1080,12 +1176,13 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     // waits for them before.  (an asm-issued load's register was
     // invisible to the compiler.)
     uint32_t pfa = 0, pfb = 0;
-    if (KSPLIT && kpos > kdone) {  // the group's last orbit keys
-      key_chunk(kdone, kpos - kdone);
+    while (KSPLIT && kpos - kdone + ccount > 0) {  // the group's last orbit keys (they key this group's rows)
+      const int kc = min(kpos - kdone, 64 - ccount);
+      key_chunk(kdone, kc, kc == 0 || kpos - kdone + ccount <= 64);  // (the last chunk: every image left)
+      kdone += kc;
       STAMP(7);
       resolve();
       issue_probe();
-      kdone = kpos;
     }
     if (gnn < ngroups) {
       const unsigned long long sn = s_begin + gnn * GROUP;
@@ -1162,6 +1259,7 @@ constexpr int compact_group(const Layout& L) {
 #define RTLA_GROUP32_LDS (19 * 1024)
 #endif
 constexpr int spec_group(const Layout& L) {
+  if (L.sym) return 16;  // configs[3]: 16 waves/CU at 128 VGPRs need the smaller tile (311.5 vs 322 ms)
   const int g = compact_group(L);
   return g == 32 && compact_lds_words(L.W, L.all_words, 32, L.sym, true) * sizeof(uint32_t) > RTLA_GROUP32_LDS ? 16 : g;
 }

@@ -9,7 +9,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 D=$ROOT/exp/$name; rm -rf $D; mkdir -p $D
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
-S=$ROOT/raft-tla_amd/csrc
+S=${SRC:-$ROOT/raft-tla_amd/csrc}  # SRC: a modified copy of csrc/ (its ../../include must hold rtla.h)
 ALL="rtla_kernels rtla_kwave rtla_kpack rtla_kspec_a rtla_kspec_b rtla_ksym_a rtla_ksym_b rtla_kgeneric_a rtla_kgeneric_b rtla_ksymkeys"
 pids=""
 if [ -n "$UNITS" ]; then
