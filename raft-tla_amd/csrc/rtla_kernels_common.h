@@ -529,9 +529,16 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
 // probe pass evaluates the full Delta of each successor and probes its orbit
 // key (successor_orbit_key) instead of its fingerprint; rows keep the states
 // themselves.
+// Waves per SIMD the level kernel's registers are budgeted for: narrow
+// compiled-in rows (<= 32 words: the exhaust model's 84 B) fit 4 (128
+// VGPRs; its 74 levels 1259 -> 1158 ms), wider ones 3 (configs[1] at 4:
+// 197.9 -> 215.6 ms, configs[2] 90.0 -> 100.0 ms; profiles/r04_v4/waves4_*).
+constexpr int compact_waves(const Layout& L, bool sym) {
+  return sym ? RTLA_SYM_WAVES_PER_EU : (L.N != 0 && L.W <= 32 ? 4 : RTLA_COMPACT_WAVES_PER_EU);
+}
 template <int NS, bool MULTI, int GROUP, Layout LC, bool SYM>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(SYM ? RTLA_SYM_WAVES_PER_EU : RTLA_COMPACT_WAVES_PER_EU)))
+__attribute__((amdgpu_waves_per_eu(compact_waves(LC, SYM))))
 k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long long s_end,
                  unsigned long long cur_base, Ring next, unsigned long long* __restrict__ parents,
                  unsigned long long next_base, unsigned long long next_cap, unsigned long long* table,
