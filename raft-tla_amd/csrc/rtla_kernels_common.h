@@ -828,7 +828,15 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           (unsigned long long)me << 56 | (cur_base + s0 + (ninfo >> 16)) << 16 | (unsigned long long)(ninfo & 0xffffu);
       const bool rem = isnew && powner != me;
       isnew = isnew && powner == me;
-      unsigned long long om = wave_or_u64(rem ? 1ull << powner : 0ull);
+      // owners with records this chunk: a ballot per owner for few shards (a
+      // wave-wide OR is a chain of 6 cross-lane exchanges per resolve)
+      unsigned long long om = 0;
+      if (box.nshard <= 8) {
+        for (int o = 0; o < box.nshard; o++)
+          if (__ballot(rem && powner == o)) om |= 1ull << o;
+      } else {
+        om = wave_or_u64(rem ? 1ull << powner : 0ull);
+      }
       while (om) {
         const int o = __builtin_ctzll(om);
         om &= om - 1;
