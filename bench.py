@@ -73,9 +73,13 @@ CAPPED = {"cfg1", "cfg2", "cfg3", "cfg4"}  # not exhaustible on one GPU
 PINNED_LEVELS = {"cfg1": 23, "cfg2": 17, "cfg3": 14, "cfg4": 15}
 DEFAULT = "cfg2"
 SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run reports it too)
-# Fingerprint-set size (log2 slots) per workload: ~25-30 % load at the size reached.
+# Fingerprint-set size (log2 slots) per workload.  configs[0]-[2]: 2^32 slots
+# (32 GiB; 7-14 % load at the pinned depth) -- fewer second-slot probes and
+# CAS misses than 2^31 (12-28 %) beat clearing twice the bytes per step
+# (configs[1] 197.2 -> 192.1 ms, configs[0] 300.9 -> 291.1, configs[2] 90.0 ->
+# 88.4; 2^33: 194.9 ms, the clear grows faster; profiles/r04_v4/fpset_*.json).
 FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30,
-              "cfg2": 31, "cfg1": 31, "cfg3": 31, "cfg4": 30, "synthetic": 33}
+              "cfg2": 32, "cfg1": 32, "cfg3": 32, "cfg4": 30, "synthetic": 33}
 # Bag slots per row for the unbounded-bag configs.  A state d BFS levels below
 # Init holds at most d - 1 distinct messages (every action adds at most one),
 # so this bounds the depth at which the row format -- not memory -- stops the
