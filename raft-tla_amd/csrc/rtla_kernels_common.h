@@ -531,14 +531,18 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
 // themselves.
 // Waves per SIMD the level kernel's registers are budgeted for: narrow
 // compiled-in rows (<= 32 words: the exhaust model's 84 B) fit 4 (128
-// VGPRs; its 74 levels 1259 -> 1158 ms), wider ones 3 (at 4: configs[1]
+// VGPRs; its 74 levels 1259 -> 1158 ms; 5 waves: 1605 ms), wider ones 3 (at 4: configs[1]
 // 197.9 -> 215.6 ms, configs[2] 90.0 -> 100.0 ms, configs[0]'s 37-word rows
 // 300.9 -> 328.0 ms; profiles/r04_v4/waves{3,4}_*).
 #ifndef RTLA_NARROW_W
-#define RTLA_NARROW_W 32  // rows of at most this many words get 4 waves/SIMD
+#define RTLA_NARROW_W 32  // rows of at most this many words get RTLA_NARROW_WAVES waves/SIMD
+#endif
+#ifndef RTLA_NARROW_WAVES
+#define RTLA_NARROW_WAVES 4
 #endif
 constexpr int compact_waves(const Layout& L, bool sym) {
-  return sym ? RTLA_SYM_WAVES_PER_EU : (L.N != 0 && L.W <= RTLA_NARROW_W ? 4 : RTLA_COMPACT_WAVES_PER_EU);
+  return sym ? RTLA_SYM_WAVES_PER_EU
+             : (L.N != 0 && L.W <= RTLA_NARROW_W ? RTLA_NARROW_WAVES : RTLA_COMPACT_WAVES_PER_EU);
 }
 template <int NS, bool MULTI, int GROUP, Layout LC, bool SYM>
 __global__ void __launch_bounds__(256)
