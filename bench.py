@@ -263,7 +263,7 @@ class Run:
                                bag_cap=BAG_CAP.get(name, 0), frontier_cap=frontier_cap,
                                symmetry=name in SYMMETRIC,
                                mem_budget=(args.mem_budget << 30) if args.mem_budget else
-                               (200 << 30) if args.shards > 1 else 0)
+                               (200 << 30) if args.shards > 1 else 0, chunk=args.chunk)
         self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
         self.levels_cap = None   # complete levels a capped search reaches
         self.pinned = PINNED_LEVELS.get(name) if args.depth == "pinned" else None
@@ -392,9 +392,7 @@ def roofline(levels, world, workload, calib=None):
         "model": "per launch: E*S rows read + 64 B per fingerprint-set probe + D*(S+8) new rows and parent records",
         "random_access": {"probes_per_s": P / world / (ems / 1e3), "ceiling_per_s": ra_ceiling,
                           "frac": P / world / (ems / 1e3) / ra_ceiling,
-                          "model": ra_model, "source": ra_source, "calibration": calib,
-                          # SURVEY.md 8(d)'s probe term: probes / (t * the calibrated random 8-B CAS rate)
-                          "frac_vs_cas_rate": P / world / (ems / 1e3) / CAS_PER_S},
+                          "model": ra_model, "source": ra_source, "calibration": calib},
     }
 
 
@@ -485,6 +483,8 @@ def main():
                          "RCCL-id payload, prints one line and exits (no GPU work; used by the CPU tests)")
     ap.add_argument("--no-calib", action="store_true",
                     help="skip the live random-access calibration (the ceiling then comes from the pure-stream model)")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="multi-shard: frontier states per shard per exchange round (0 = sized from the budget)")
     ap.add_argument("--shards", type=int, default=0,
                     help="diagnostic: split the search on one GPU into this many fingerprint-owned shards "
                          "(the multi-GPU exchange protocol with device copies as transport)")
@@ -609,6 +609,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "BFS from the Init row (no input data)" + (
+            (", the oracle-pinned depth (%d complete levels, every level's counts and state set in "
+             "tests/golden/bfs_counts.json)" % run.levels_cap) if run.capped and run.pinned and not args.cap_levels else
+            (", %d complete levels (--cap-levels)" % run.levels_cap) if run.capped and args.cap_levels else
             ", capped at the deepest level that fits device memory" if run.capped else ", exhaustive"),
         "config": config,
         "cpu_baseline": None,

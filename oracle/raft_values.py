@@ -815,3 +815,32 @@ def level_text_hashes(cfg: Cfg, max_states: Optional[int] = None) -> List[int]:
         if max_states and len(seen) > max_states:
             raise RuntimeError("state budget exceeded")
     return out
+
+
+def bfs_prefix(cfg: Cfg, max_levels: int, symmetric: bool = False) -> Tuple[List[Tuple[int, int]], List[int]]:
+    """The first `max_levels` BFS levels (Init = level 1): per level (new,
+    generated) and its content digest -- the sum mod 2^64 of FNV-1a over the
+    new states' texts, or (symmetric: SYMMETRY Permutations(Server)) over the
+    new orbits' orbit texts.  The same conventions as bfs / bfs_symmetric, cut
+    after a level count instead of run to exhaustion: pins the C oracle's
+    fixtures of the BASELINE configs (which no oracle exhausts) on their
+    first levels (tests/golden/make_golden.py PY_PINS)."""
+    s0 = init_state(cfg)
+    key = (lambda t: orbit_key(cfg, t)) if symmetric else (lambda t: t)
+    text = (lambda t: orbit_text(cfg, t)) if symmetric else (lambda t: state_text(cfg, t))
+    seen = {key(s0)}
+    levels, hashes, frontier = [(1, 1)], [fnv1a64(text(s0))], [s0]
+    while frontier and len(levels) < max_levels:
+        nxt, gen = [], 0
+        for s in frontier:
+            for _lab, t in next_states(cfg, s):
+                gen += 1
+                if in_model(cfg, t):
+                    k = key(t)
+                    if k not in seen:
+                        seen.add(k)
+                        nxt.append(t)
+        levels.append((len(nxt), gen))
+        hashes.append(sum(fnv1a64(text(t)) for t in nxt) & 0xFFFFFFFFFFFFFFFF)
+        frontier = nxt
+    return levels, hashes

@@ -19,6 +19,7 @@ enum {
   FLAG_FPSET_FULL = 8,      // fingerprint set probe limit hit
   FLAG_OUTBOX_FULL = 16,    // exchange outbox region too small
   FLAG_BAD_INDEX = 32,      // RTLA_CHECKED builds: a global index outside its buffer
+  FLAG_LOCAL_FAILURE = 64,  // (host) a rank's local work failed: carried to every rank in the level reduction
 };
 static_assert(FLAG_SPEC_ERROR == RTLA_CAP_SPEC_ERROR && FLAG_ROW_OVERFLOW == RTLA_CAP_ROW &&
                   FLAG_FRONTIER_FULL == RTLA_CAP_FRONTIER && FLAG_FPSET_FULL == RTLA_CAP_FPSET &&
@@ -29,6 +30,8 @@ static_assert(FLAG_SPEC_ERROR == RTLA_CAP_SPEC_ERROR && FLAG_ROW_OVERFLOW == RTL
 // one device): the expand kernels keep per-owner outbox state in registers /
 // LDS sized by it, and rtla_open refuses more (RTLA_E_CONFIG).
 constexpr int SHARD_MAX = 8;
+// Outbox slots a wave of the level kernel reserves per owner at a time.
+constexpr int OBOX_CHUNK = 256;
 
 // Fingerprint ownership across shards (ranks): low 32 bits of fp.a scaled to
 // [0, nshard).  The fingerprint-set home slot uses the TOP bits of fp.a, so
@@ -52,15 +55,24 @@ RTLA_HD unsigned long long ring_idx(const Ring& r, unsigned long long g) {
   return i >= r.cap ? i - r.cap : i;
 }
 
-// Outbox of one shard for one expansion chunk: region p (capacity `cap`
-// records) holds the successors owned by shard p.
+// Outbox of one shard for one exchange round: region p (capacity `cap`
+// records) holds the successors owned by shard p.  The level kernel stops
+// taking frontier groups once any region holds `stop_at` records; what the
+// groups already in flight still queue past a region's end goes to the
+// overflow list (owner mixed, sent in the next round).  The overflow's
+// capacity covers every in-flight group queueing all its candidates.
 struct ShardBox {
   int nshard, me;
   unsigned long long cap;
-  int slog2;                      // log2 slots of the sent cache (MULTI)
+  int slog2;                      // log2 slots of the sent cache (MULTI; 0 = no sent cache)
   unsigned long long* out_count;  // [nshard]
   unsigned long long* send_fp;    // [nshard][cap][2]
   unsigned long long* send_ref;   // [nshard][cap]: local parent index << 16 | instance
+  unsigned long long stop_at;     // k_expand_compact: no new group once a region holds this many
+  unsigned long long* over_fp;    // [over_cap][2]: records past their region's end
+  unsigned long long* over_ref;   // [over_cap]
+  unsigned long long* over_count; // its fill counter
+  unsigned long long over_cap;
 };
 
 // Diagnostic switches of the expand kernels (rtla_time_expand, RTLA_XFLAGS; 0 in the BFS).
@@ -81,9 +93,6 @@ enum {
   XF_ALL_SUCCESSORS = 16384,  // compact kernel: no seen set -- every enabled successor (in-model or not) gets a
                               // row, its record = input index << 32 | in_model << 31 | sub << 16 | instance
                               // (rtla_expand_batch: the parity seam runs the hot kernel)
-  XF_SYM_QUEUE = 32768,   // SYMMETRY, one shard (set by the driver): the compact kernel only evaluates and
-                          // queues (parent << 16 | instance) of the successors that need an orbit key into
-                          // box.send_ref[0, box.cap) (fill counter *box.out_count); k_sym_keys keys them
 };
 
 // Per-level device counters (zeroed before each level except `cover`).
@@ -98,6 +107,7 @@ struct DevCounters {
   unsigned long long viol_parent;
   unsigned long long viol_child;
   unsigned long long group_next;  // k_expand_compact's work queue (zeroed before each launch)
+  unsigned long long group_size;  // frontier states per group of the last k_expand_compact launch
   unsigned long long stamp[8];    // RTLA_STAMPS builds: cycles per level-kernel phase, summed over waves
   unsigned long long cas;         // RTLA_COUNT_CAS builds: pipelined fingerprint-set CAS issued by the level kernel
   // buffer capacities (rows of the current / next frontier, parent records), for RTLA_CHECKED builds

@@ -24,23 +24,24 @@
 //                             broadcasts): the RCCL call sites of the
 //                             multi-GPU path execute on a one-GPU box.
 //
-// Multi-shard level (per chunk of the frontier, all shards in lock-step):
-//   1. k_expand: successors owned locally are probed/inserted/materialised at
-//      once; the others are queued as (fp, parent, instance) per owner;
-//   2. all-gather of the per-destination counts, then all-to-all-v of the
+// Multi-shard level: exchange rounds, all shards in lock-step (rtla_step):
+//   1. k_expand_compact: successors owned locally are probed, inserted and
+//      built at once; the others are queued as (fingerprint, parent ref) per
+//      owner.  The kernel expands the rest of the frontier until an owner's
+//      outbox region fills (its group guard), so a round is as large as the
+//      outbox allows;
+//   2. all-gather of the per-owner counts (+ what each shard has left) --
+//      the round's only host synchronisation -- then all-to-all-v of the
 //      16-byte fingerprints (ncclSend/ncclRecv pairs in one group: all 7 xGMI
 //      links of an MI355X node carry traffic at once);
-//   3. k_insert_remote at the owner answers each record with 0 (seen) or
-//      1 + a dense rank among the new fingerprints from that sender;
-//   4. all-to-all-v of the answers back, all-gather of the winner counts;
-//   5. k_pack_rows at the sender materialises the winners (it holds the
-//      parent row) into the owner's row region at their rank, one all-to-all-v
-//      ships the rows, k_unpack_rows appends them to the owner's next
-//      frontier.  New states therefore live on their owner shard, which
-//      spreads the next level's expansion evenly; parent records name the
-//      parent's shard, so traces walk across shards.
+//   3. k_insert_remote at the owner answers each record new / seen;
+//   4. all-to-all-v of the answers back;
+//   5. k_build_winners: each sender builds the rows of its winners into its
+//      own next level (rows never cross shards; parent records name the
+//      parent's shard, so traces walk across shards).
 // Then one all-reduce of {new, generated, probes, violation, flags} decides
-// termination (TLC's "0 states left on queue").
+// termination (TLC's "0 states left on queue"), and the next levels are
+// re-balanced where they drifted from an even split.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -79,9 +80,10 @@ struct Shard {
   DevCounters* ctr = nullptr;
   int* dflags = nullptr;
   // exchange buffers (nshard > 1)
-  uint64_t* out_count = nullptr;   // [G] device: records queued per destination
+  uint64_t* out_count = nullptr;   // [G + 2] device: records queued per destination (reserved slots; those past
+                                   // box_cap are on the overflow list), frontier states left, overflow records
   uint64_t* in_count = nullptr;    // [G] device: records received per source
-  uint64_t* all_count = nullptr;   // [G][G] device (RCCL all-gather target)
+  uint64_t* all_count = nullptr;   // [G][G + 2] device (RCCL all-gather target)
   uint64_t* send_fp = nullptr;     // [G][cap][2]
   uint64_t* send_ref = nullptr;    // [G][cap]
   uint32_t* send_ans = nullptr;    // [G][cap]  owners' answers to our records
@@ -92,11 +94,13 @@ struct Shard {
   uint32_t* send_rows = nullptr;   // [G][rows_cap][W + 2]  re-balancing staging
   uint32_t* recv_rows = nullptr;   // [G][rows_cap][W + 2]
   uint64_t* sent = nullptr;        // [2^slog2] sent cache: fingerprints this shard already sent to their owners
+  uint64_t* over_fp[2] = {nullptr, nullptr};   // overflow lists [over_cap][2]: records past their region's end,
+  uint64_t* over_ref[2] = {nullptr, nullptr};  // sent in the next round (k_requeue)
+  uint64_t* over_cnt = nullptr;    // [2] their lengths
+  int ov = 0;                      // the list the next round requeues
+  uint64_t pos = 0, over_n = 0;    // this level: next frontier state to expand, records on list ov
   std::vector<uint64_t> h_out, h_in, h_all;
   uint64_t h_reb[2 * SHARD_MAX] = {};  // re-balancing: rows_in / rows_base of this sub-round (host staging)
-  // SYMMETRY, one shard: the key queue between the level kernel and k_sym_keys
-  uint64_t* queue = nullptr;        // [qcap] parent << 16 | instance (~0 = hole)
-  uint64_t* qcount = nullptr;       // its fill counter
   uint64_t h_caps[3] = {0, 0, 0};  // -> DevCounters cap_cur / cap_next / cap_parents
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   // violation found on this shard
@@ -116,6 +120,7 @@ struct Shard {
 struct ShmComm {
   struct Header {
     std::atomic<uint32_t> arrive, gen;
+    std::atomic<uint32_t> abort;  // a rank failed inside a collective: every wait ends (RTLA_E_COMM)
   };
   Header* hdr = nullptr;
   uint8_t* data = nullptr;   // world x world slots of `slot` bytes: [src][dst]
@@ -137,8 +142,12 @@ struct rtla_ctx {
   int tlog2 = 0;
   int slog2 = 0;           // sent cache: 2^slog2 slots per shard (multi-shard)
   uint64_t front_cap = 0, box_cap = 0, chunk = 0, rows_cap = 0;
+  uint64_t stop_at = 0, over_cap = 0;  // multi-shard outbox: the level kernel's group guard, overflow list capacity
+  bool guarded = false;    // multi-shard rounds run the grouped level kernel (rounds sized by the outbox)
+  std::vector<uint64_t> h_rows;  // [G][G + 2] the round's gathered counts, every shard's row
   uint64_t rebalanced = 0; // rows moved by level-end re-balancing (all levels, this process's shards)
-  uint64_t qcap = 0, qchunk = 0;  // SYMMETRY key queue: entries, frontier states per round (0: keys in the level kernel)
+  uint64_t rounds = 0;     // exchange rounds run (all levels)
+  uint64_t overflowed = 0; // records that went through the overflow list (all levels, this process's shards)
   uint64_t* red = nullptr;  // device scratch for all-reduces
   int level = 0;
   bool inited = false, finished = false;
@@ -199,6 +208,7 @@ static hipError_t ring_copy(const Ring& r, int W, uint64_t g, uint64_t n, uint32
 
 static int shm_barrier(rtla_ctx* x) {
   ShmComm::Header* h = x->shm->hdr;
+  if (h->abort.load(std::memory_order_acquire)) return RTLA_E_COMM;
   const uint32_t g = h->gen.load(std::memory_order_acquire);
   if (h->arrive.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)x->world - 1) {
     h->arrive.store(0, std::memory_order_relaxed);
@@ -207,6 +217,10 @@ static int shm_barrier(rtla_ctx* x) {
   }
   const auto t0 = std::chrono::steady_clock::now();
   while (h->gen.load(std::memory_order_acquire) == g) {
+    if (h->abort.load(std::memory_order_acquire)) {
+      fprintf(stderr, "rtla: shm transport: another rank failed inside a collective\n");
+      return RTLA_E_COMM;
+    }
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) {
       fprintf(stderr, "rtla: shm transport: the other ranks did not arrive\n");
       return RTLA_E_COMM;
@@ -244,22 +258,42 @@ static int shm_open_comm(rtla_ctx* x, const void* comm_id) {
   return rc;
 }
 
+static int shm_fail(const ShmComm& c, int rc) {  // a local failure inside a collective: the peers' waits end too
+  c.hdr->abort.store(1, std::memory_order_release);
+  return rc;
+}
+
 static int shm_too_big(size_t bytes, const ShmComm& c) {
   if (bytes <= c.slot) return RTLA_OK;
   fprintf(stderr, "rtla: shm transport: %zu-byte message exceeds the %zu-byte slot (RTLA_SHM_SLOT_MB)\n", bytes, c.slot);
+  return shm_fail(c, RTLA_E_COMM);
+}
+
+// A HIP call inside an shm collective: on failure mark the abort before returning.
+#define SHMCHK(c, x)                                                                                \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) {                                                                         \
+      fprintf(stderr, "rtla: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return shm_fail((c), RTLA_E_HIP);                                                             \
+    }                                                                                               \
+  } while (0)
+
+static int nccl_fail(ncclResult_t r, int line) {
+  fprintf(stderr, "rtla: RCCL error %s at %s:%d\n", ncclGetErrorString(r), __FILE__, line);
   return RTLA_E_COMM;
 }
 
 // In place: sum (op 0) or max (op 1) of n u64 over all ranks.
 static int comm_allreduce(rtla_ctx* x, uint64_t* buf, int n, int op) {
   if (!x->shm) {
-    NCCLCHK(ncclAllReduce(buf, buf, n, ncclUint64, op ? ncclMax : ncclSum, x->comm, x->stream));
-    return RTLA_OK;
+    const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclUint64, op ? ncclMax : ncclSum, x->comm, x->stream);
+    return r == ncclSuccess ? RTLA_OK : nccl_fail(r, __LINE__);
   }
   const ShmComm& c = *x->shm;
   if (int rc = shm_too_big(8 * (size_t)n, c)) return rc;
-  HIPCHK(hipMemcpyAsync(c.slot_at(x->rank, 0, x->world), buf, 8 * n, hipMemcpyDeviceToHost, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
+  SHMCHK(c, hipMemcpyAsync(c.slot_at(x->rank, 0, x->world), buf, 8 * n, hipMemcpyDeviceToHost, x->stream));
+  SHMCHK(c, hipStreamSynchronize(x->stream));
   if (int rc = shm_barrier(x)) return rc;
   std::vector<uint64_t> acc(n, 0);
   for (int r = 0; r < x->world; r++) {
@@ -267,49 +301,50 @@ static int comm_allreduce(rtla_ctx* x, uint64_t* buf, int n, int op) {
     for (int i = 0; i < n; i++) acc[i] = op ? std::max(acc[i], v[i]) : acc[i] + v[i];
   }
   if (int rc = shm_barrier(x)) return rc;
-  HIPCHK(hipMemcpyAsync(buf, acc.data(), 8 * n, hipMemcpyHostToDevice, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
+  SHMCHK(c, hipMemcpyAsync(buf, acc.data(), 8 * n, hipMemcpyHostToDevice, x->stream));
+  SHMCHK(c, hipStreamSynchronize(x->stream));
   return RTLA_OK;
 }
 
 // recv[r * n + i] = send[i] of rank r.
 static int comm_allgather(rtla_ctx* x, const uint64_t* send, uint64_t* recv, int n) {
   if (!x->shm) {
-    NCCLCHK(ncclAllGather(send, recv, n, ncclUint64, x->comm, x->stream));
-    return RTLA_OK;
+    const ncclResult_t r = ncclAllGather(send, recv, n, ncclUint64, x->comm, x->stream);
+    return r == ncclSuccess ? RTLA_OK : nccl_fail(r, __LINE__);
   }
   const ShmComm& c = *x->shm;
   if (int rc = shm_too_big(8 * (size_t)n, c)) return rc;
-  HIPCHK(hipMemcpyAsync(c.slot_at(x->rank, 0, x->world), send, 8 * n, hipMemcpyDeviceToHost, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
+  SHMCHK(c, hipMemcpyAsync(c.slot_at(x->rank, 0, x->world), send, 8 * n, hipMemcpyDeviceToHost, x->stream));
+  SHMCHK(c, hipStreamSynchronize(x->stream));
   if (int rc = shm_barrier(x)) return rc;
   for (int r = 0; r < x->world; r++)
-    HIPCHK(hipMemcpyAsync(recv + (size_t)r * n, c.slot_at(r, 0, x->world), 8 * n, hipMemcpyHostToDevice, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
+    SHMCHK(c, hipMemcpyAsync(recv + (size_t)r * n, c.slot_at(r, 0, x->world), 8 * n, hipMemcpyHostToDevice, x->stream));
+  SHMCHK(c, hipStreamSynchronize(x->stream));
   return shm_barrier(x);
 }
 
 static int comm_bcast(rtla_ctx* x, uint64_t* buf, int n, int root) {
   if (!x->shm) {
-    NCCLCHK(ncclBroadcast(buf, buf, n, ncclUint64, root, x->comm, x->stream));
-    return RTLA_OK;
+    const ncclResult_t r = ncclBroadcast(buf, buf, n, ncclUint64, root, x->comm, x->stream);
+    return r == ncclSuccess ? RTLA_OK : nccl_fail(r, __LINE__);
   }
   const ShmComm& c = *x->shm;
   if (int rc = shm_too_big(8 * (size_t)n, c)) return rc;
   if (x->rank == root) {
-    HIPCHK(hipMemcpyAsync(c.slot_at(root, 0, x->world), buf, 8 * n, hipMemcpyDeviceToHost, x->stream));
-    HIPCHK(hipStreamSynchronize(x->stream));
+    SHMCHK(c, hipMemcpyAsync(c.slot_at(root, 0, x->world), buf, 8 * n, hipMemcpyDeviceToHost, x->stream));
+    SHMCHK(c, hipStreamSynchronize(x->stream));
   }
   if (int rc = shm_barrier(x)) return rc;
   if (x->rank != root) {
-    HIPCHK(hipMemcpyAsync(buf, c.slot_at(root, 0, x->world), 8 * n, hipMemcpyHostToDevice, x->stream));
-    HIPCHK(hipStreamSynchronize(x->stream));
+    SHMCHK(c, hipMemcpyAsync(buf, c.slot_at(root, 0, x->world), 8 * n, hipMemcpyHostToDevice, x->stream));
+    SHMCHK(c, hipStreamSynchronize(x->stream));
   }
   return shm_barrier(x);
 }
 
 // One all-to-all-v round: point-to-point messages (at most one send and one
-// receive per peer), all in flight together (one RCCL group).
+// receive per peer), all in flight together (one RCCL group).  The group is
+// always closed, also when a send or receive could not be posted.
 struct Msg {
   void* ptr;
   size_t bytes;
@@ -317,24 +352,28 @@ struct Msg {
 };
 static int comm_exchange(rtla_ctx* x, const std::vector<Msg>& sends, const std::vector<Msg>& recvs) {
   if (!x->shm) {
-    NCCLCHK(ncclGroupStart());
-    for (const Msg& m : sends) NCCLCHK(ncclSend(m.ptr, m.bytes, ncclUint8, m.peer, x->comm, x->stream));
-    for (const Msg& m : recvs) NCCLCHK(ncclRecv(m.ptr, m.bytes, ncclUint8, m.peer, x->comm, x->stream));
-    NCCLCHK(ncclGroupEnd());
-    return RTLA_OK;
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return nccl_fail(r, __LINE__);
+    for (const Msg& m : sends)
+      if (r == ncclSuccess) r = ncclSend(m.ptr, m.bytes, ncclUint8, m.peer, x->comm, x->stream);
+    for (const Msg& m : recvs)
+      if (r == ncclSuccess) r = ncclRecv(m.ptr, m.bytes, ncclUint8, m.peer, x->comm, x->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    return r == ncclSuccess ? RTLA_OK : nccl_fail(r, __LINE__);
   }
   const ShmComm& c = *x->shm;
   for (const Msg& m : sends) {
     if (int rc = shm_too_big(m.bytes, c)) return rc;
-    HIPCHK(hipMemcpyAsync(c.slot_at(x->rank, m.peer, x->world), m.ptr, m.bytes, hipMemcpyDeviceToHost, x->stream));
+    SHMCHK(c, hipMemcpyAsync(c.slot_at(x->rank, m.peer, x->world), m.ptr, m.bytes, hipMemcpyDeviceToHost, x->stream));
   }
-  HIPCHK(hipStreamSynchronize(x->stream));
+  SHMCHK(c, hipStreamSynchronize(x->stream));
   if (int rc = shm_barrier(x)) return rc;
   for (const Msg& m : recvs) {
     if (int rc = shm_too_big(m.bytes, c)) return rc;
-    HIPCHK(hipMemcpyAsync(m.ptr, c.slot_at(m.peer, x->rank, x->world), m.bytes, hipMemcpyHostToDevice, x->stream));
+    SHMCHK(c, hipMemcpyAsync(m.ptr, c.slot_at(m.peer, x->rank, x->world), m.bytes, hipMemcpyHostToDevice, x->stream));
   }
-  HIPCHK(hipStreamSynchronize(x->stream));
+  SHMCHK(c, hipStreamSynchronize(x->stream));
   return shm_barrier(x);
 }
 
@@ -587,6 +626,7 @@ extern "C" int rtla_orbit_text(const rtla_cfg* c, const uint32_t* row, char* buf
 }
 
 static int flags_to_status(int flags) {
+  if (flags & FLAG_LOCAL_FAILURE) return RTLA_E_HIP;
   if (flags & FLAG_SPEC_ERROR) return RTLA_E_SPEC;
   if (flags) return RTLA_E_OVERFLOW;
   return RTLA_OK;
@@ -597,8 +637,9 @@ static void report_flags(int flags) {
   if (flags & FLAG_ROW_OVERFLOW) fprintf(stderr, "rtla: row capacity exceeded (raise bag_cap / elec_cap)\n");
   if (flags & FLAG_FRONTIER_FULL) fprintf(stderr, "rtla: next-frontier buffer full (raise frontier_cap / mem_budget)\n");
   if (flags & FLAG_FPSET_FULL) fprintf(stderr, "rtla: fingerprint set too full (raise fpset_log2)\n");
-  if (flags & FLAG_OUTBOX_FULL) fprintf(stderr, "rtla: exchange outbox full (lower chunk)\n");
+  if (flags & FLAG_OUTBOX_FULL) fprintf(stderr, "rtla: exchange outbox overflow list full\n");
   if (flags & FLAG_BAD_INDEX) fprintf(stderr, "rtla: checked build: a kernel index left its buffer\n");
+  if (flags & FLAG_LOCAL_FAILURE) fprintf(stderr, "rtla: a rank's local work failed\n");
 }
 
 // RTLA_XFLAGS: kernel-variant switches (XF_* in rtla_device.h) for performance
@@ -762,7 +803,8 @@ extern "C" int rtla_comm_id(void* out128) {
 static void free_shard(Shard& s) {
   void* ptrs[] = {s.table,    s.sent,     s.parents,  s.arena,    s.ctr,       s.dflags,    s.out_count,
                   s.in_count, s.all_count, s.send_fp, s.send_ref, s.send_ans,  s.recv_fp,   s.recv_ans,
-                  s.rows_in,  s.rows_base, s.send_rows, s.recv_rows, s.queue, s.qcount};
+                  s.rows_in,  s.rows_base, s.send_rows, s.recv_rows, s.over_fp[0], s.over_fp[1],
+                  s.over_ref[0], s.over_ref[1], s.over_cnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -793,12 +835,11 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   uint64_t pbytes = s.parents_cap * 8;
   uint64_t rowb = (uint64_t)L.W * 4;
   uint64_t boxb = G > 1 ? (uint64_t)G * x->box_cap * (16 + 8 + 4 + 16 + 4) +
-                              2ull * G * x->rows_cap * (L.W + 2) * 4
+                              2ull * G * x->rows_cap * (L.W + 2) * 4 + 2ull * x->over_cap * 24
                         : 0;
-  const uint64_t sbytes = G > 1 ? 8ull << x->slog2 : 0;
-  const uint64_t qbytes = 8 * x->qcap;
+  const uint64_t sbytes = G > 1 && x->slog2 ? 8ull << x->slog2 : 0;
   if (!x->front_cap) {
-    uint64_t used = tbytes + sbytes + pbytes + boxb + qbytes;
+    uint64_t used = tbytes + sbytes + pbytes + boxb;
     uint64_t rest = budget > used ? budget - used : 0;
     x->front_cap = std::max<uint64_t>(rest / rowb, 2048);
   }
@@ -809,9 +850,9 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   HIPCHK(hipMalloc(&s.ctr, sizeof(DevCounters)));
   HIPCHK(hipMalloc(&s.dflags, sizeof(int) * 64));
   if (G > 1) {
-    HIPCHK(hipMalloc(&s.out_count, 8 * G));
+    HIPCHK(hipMalloc(&s.out_count, 8 * (G + 2)));
     HIPCHK(hipMalloc(&s.in_count, 8 * G));
-    HIPCHK(hipMalloc(&s.all_count, 8 * G * G));
+    HIPCHK(hipMalloc(&s.all_count, 8 * G * (G + 2)));
     HIPCHK(hipMalloc(&s.send_fp, 16 * G * x->box_cap));
     HIPCHK(hipMalloc(&s.send_ref, 8 * G * x->box_cap));
     HIPCHK(hipMalloc(&s.send_ans, 4 * G * x->box_cap));
@@ -821,21 +862,88 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
     HIPCHK(hipMalloc(&s.rows_base, 8 * G));
     HIPCHK(hipMalloc(&s.send_rows, 4ull * G * x->rows_cap * (L.W + 2)));
     HIPCHK(hipMalloc(&s.recv_rows, 4ull * G * x->rows_cap * (L.W + 2)));
-    s.h_out.assign(G, 0);
+    for (int k = 0; k < 2; k++) {
+      HIPCHK(hipMalloc(&s.over_fp[k], 16 * std::max<uint64_t>(x->over_cap, 1)));
+      HIPCHK(hipMalloc(&s.over_ref[k], 8 * std::max<uint64_t>(x->over_cap, 1)));
+    }
+    HIPCHK(hipMalloc(&s.over_cnt, 16));
+    HIPCHK(hipMemsetAsync(s.over_cnt, 0, 16, x->stream));
+    s.h_out.assign(G + 2, 0);
     s.h_in.assign(G, 0);
-    s.h_all.assign((size_t)G * G, 0);
-    HIPCHK(hipMalloc(&s.sent, sbytes));
-    HIPCHK(hipMemsetAsync(s.sent, 0, sbytes, x->stream));
-  }
-  if (x->qcap) {
-    HIPCHK(hipMalloc(&s.queue, qbytes));
-    HIPCHK(hipMalloc(&s.qcount, 8));
+    s.h_all.assign((size_t)G * (G + 2), 0);
+    if (sbytes) {
+      HIPCHK(hipMalloc(&s.sent, sbytes));
+      HIPCHK(hipMemsetAsync(s.sent, 0, sbytes, x->stream));
+    }
   }
   HIPCHK(hipMemsetAsync(s.table, 0, tbytes, x->stream));
   HIPCHK(hipMemsetAsync(s.ctr, 0, sizeof(DevCounters), x->stream));
   HIPCHK(hipEventCreate(&s.ev0));
   HIPCHK(hipEventCreate(&s.ev1));
   HIPCHK(hipEventCreate(&s.evm));
+  return RTLA_OK;
+}
+
+// RTLA_FAULT=<where>:<rank> (tests): this rank's local work at <where> fails,
+// so the tests can check that the failure reaches every rank promptly.
+static bool fault_here(const rtla_ctx* x, const char* where) {
+  const char* e = getenv("RTLA_FAULT");
+  if (!e) return false;
+  const char* colon = strchr(e, ':');
+  if (!colon || (size_t)(colon - e) != strlen(where) || strncmp(e, where, colon - e) != 0) return false;
+  return atoi(colon + 1) == x->rank;
+}
+
+// Sum (op 0) or max (op 1) of n u64 over all ranks; host in/out.
+static int allreduce_u64(rtla_ctx* x, uint64_t* v, int n, int op);
+
+// Multi-shard exchange sizing.  Per owner, an outbox region
+// of box_cap records (48 B each with the answers and the receiving side):
+// ~1/12 of the budget over the G regions.  The level kernel takes frontier
+// groups while every region is below stop_at; the groups in flight when one
+// fills -- at most one per resident wave, each of whose GROUP states may
+// queue every action instance -- spill onto the overflow list (over_cap).
+// Without the group queue (the wave-per-state kernel) a round is bounded
+// instead, so that no region can overflow (chunk).  Every rank must agree on
+// these (round counts and message sizes follow from them): world > 1 takes
+// the smallest of each over the ranks.
+static int size_exchange(rtla_ctx* x, uint64_t per) {
+  const Layout& L = x->L;
+  const int G = x->nshard;
+  const uint64_t ninst = (uint64_t)L.fam[F_COUNT];  // records one frontier state queues at most
+  int waves = 0, group = 0;
+  x->guarded = level_kernel_shape(L, true, env_xflags(), &waves, &group);
+  x->box_cap = std::max<uint64_t>(per / 12 / ((uint64_t)G * 48), 16 * OBOX_CHUNK);
+  if (const char* e = getenv("RTLA_OUTBOX_CAP"))  // tests: tiny regions, many rounds, the overflow list in use
+    if (atoll(e) > 0) x->box_cap = std::max<uint64_t>((uint64_t)atoll(e), 16 * OBOX_CHUNK);
+  if (x->cfg.chunk) x->chunk = round64(x->cfg.chunk);  // explicit bound on the states a round expands
+  else x->chunk = x->guarded ? 0 : std::max<uint64_t>(64, (x->box_cap / ninst) & ~63ull);
+  x->over_cap = x->guarded ? (uint64_t)waves * (uint64_t)group * ninst : 0;
+  // the two overflow lists (24 B a record) take at most 1/16 of the budget: a
+  // small budget bounds the states a round expands instead, so that even
+  // then every record of a launch would fit the list
+  const uint64_t over_room = std::max<uint64_t>(per / 16 / 48, 64 * ninst);
+  if (x->over_cap > over_room) {
+    x->over_cap = over_room;
+    const uint64_t c = std::max<uint64_t>(64, (over_room / ninst) & ~63ull);
+    x->chunk = x->chunk ? std::min(x->chunk, c) : c;
+  }
+  // re-balancing staging: ~1/20 of the budget; more rows move in sub-rounds
+  x->rows_cap = (per / 20) / (2ull * G * (L.W + 2) * 4);
+  x->rows_cap = std::min<uint64_t>(std::max<uint64_t>(x->rows_cap, 256), x->box_cap);
+  if (x->world > 1) {  // min over the ranks (max of the complements); the overflow bound: max
+    uint64_t v[5] = {~x->box_cap, ~(x->chunk ? x->chunk : ~0ull), ~x->rows_cap, x->over_cap, x->guarded ? 0ull : 1ull};
+    if (int rc = allreduce_u64(x, v, 5, 1)) return rc;
+    x->box_cap = ~v[0];
+    x->chunk = ~v[1] == ~0ull ? 0 : ~v[1];
+    x->rows_cap = ~v[2];
+    x->over_cap = v[3];
+    if (v[4] && x->guarded) {  // some rank runs the wave-per-state kernel: all bound their rounds alike
+      x->guarded = false;
+      if (!x->chunk) x->chunk = std::max<uint64_t>(64, (x->box_cap / ninst) & ~63ull);
+    }
+  }
+  x->stop_at = x->box_cap - std::max<uint64_t>(x->box_cap / 8, OBOX_CHUNK);
   return RTLA_OK;
 }
 
@@ -859,6 +967,7 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   int nlocal = world > 1 ? 1 : x->nshard;
   if (hipSetDevice(x->device) != hipSuccess) { delete x; return RTLA_E_HIP; }
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) { delete x; return RTLA_E_HIP; }
+  if (hipMalloc(&x->red, 64 * 8) != hipSuccess) { rtla_close(x); return RTLA_E_HIP; }
   if (world > 1) {
     const char* tr = getenv("RTLA_TRANSPORT");
     if (tr && !strcmp(tr, "shm")) {
@@ -890,27 +999,17 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
       x->rccl_local = true;
     }
   }
+  // From here on (world > 1) every rank reaches the same collectives: a local
+  // failure is carried to the last one, which fails every rank together.
+  int err = RTLA_OK;
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
   uint64_t budget = cfg->mem_budget ? cfg->mem_budget : (uint64_t)(free_b * 0.85);
   uint64_t per = budget / nlocal;
   const Layout& L = x->L;
   const int G = x->nshard;
-  // exchange sizing: one frontier state queues at most (fixed + 3 * bag_cap)
-  // records, all possibly for the same destination
-  if (G > 1) {
-    uint64_t nmax = (uint64_t)(L.fam[F_RECEIVE] + 3 * L.K);
-    x->chunk = cfg->chunk;
-    if (!x->chunk) {
-      x->chunk = (per / 8) / ((uint64_t)G * nmax * 48);
-      x->chunk = std::min<uint64_t>(std::max<uint64_t>(x->chunk, 1024), 4u << 20);
-    }
-    x->chunk = round64(x->chunk);  // exchange rounds start at 64-row group boundaries (Ring)
-    x->box_cap = x->chunk * nmax;
-    // re-balancing staging: ~1/20 of the budget; more rows move in sub-rounds
-    x->rows_cap = (per / 20) / (2ull * G * (L.W + 2) * 4);
-    x->rows_cap = std::min<uint64_t>(std::max<uint64_t>(x->rows_cap, 256), x->box_cap);
-  }
+  if (G > 1)
+    if (int rc = size_exchange(x, per)) { rtla_close(x); return rc; }
   int tl = cfg->fpset_log2;
   if (!tl) {
     tl = 20;
@@ -918,39 +1017,32 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
     const uint64_t tshare = G > 1 ? per * 8 / 25 : per * 2 / 5;
     while (tl < 34 && (8ull << (tl + 1)) <= tshare) tl++;
   }
-  if (tl < 10 || tl > 40) { rtla_close(x); return RTLA_E_CONFIG; }
+  if (tl < 10 || tl > 40) err = RTLA_E_CONFIG;
   x->tlog2 = tl;
   // the sent cache is a dedup hint (one slot per fingerprint, overwritten on
-  // a miss): a quarter of the set's slots
-  x->slog2 = std::max(12, tl - 2);
-  // SYMMETRY on one shard: orbit keys in a kernel of their own (k_sym_keys),
-  // fed by a queue of (parent, instance) entries ~1/16 of the budget; the
-  // level runs in rounds of frontier states whose successors surely fit it
-  // (every instance enabled, a quarter lost to chunk holes)
-  if (L.sym && G == 1 && expand_compact_wpb(L) > 0 && launch_sym_keys_supported(L)) {
-    const char* q = getenv("RTLA_SYM_QUEUE");  // opt-in: measured slower than keys in the level kernel
-    if (q && atoi(q) != 0) {
-      x->qcap = std::min<uint64_t>(per / 16 / 8, 1ull << 31);
-      const uint64_t holes = 256ull * 4096;  // a 256-entry chunk open per resident wave
-      const uint64_t usable = x->qcap > 2 * holes ? (x->qcap - holes) * 3 / 4 : 0;
-      x->qchunk = usable / (uint64_t)L.fam[F_COUNT] & ~63ull;
-      if (x->qchunk < 64) x->qcap = x->qchunk = 0;
-    }
-  }
+  // a miss): a quarter of the set's slots; RTLA_SENT_CACHE=0 turns it off
+  // (every remote successor is queued for its owner)
+  const char* sc = getenv("RTLA_SENT_CACHE");
+  x->slog2 = sc && atoi(sc) == 0 ? 0 : std::max(12, tl - 2);
   x->front_cap = cfg->frontier_cap;
   x->sh.resize(nlocal);
-  for (int k = 0; k < nlocal; k++) {
+  for (int k = 0; k < nlocal && !err; k++) {
     x->sh[k].id = x->shard0 + k;
     if (alloc_shard(x, x->sh[k], per) != RTLA_OK) {
       fprintf(stderr, "rtla: device allocation failed (fpset 2^%d slots, frontier 2x%llu rows of %d B)\n", tl,
               (unsigned long long)x->front_cap, L.W * 4);
-      rtla_close(x);
-      return RTLA_E_HIP;
+      err = RTLA_E_HIP;
     }
   }
-  if (hipMalloc(&x->red, 64 * 8) != hipSuccess || hipStreamSynchronize(x->stream) != hipSuccess) {
+  if (!err && (hipStreamSynchronize(x->stream) != hipSuccess || fault_here(x, "open"))) err = RTLA_E_HIP;
+  if (world > 1) {  // every rank opened, or none
+    uint64_t bad = err ? 1 : 0;
+    if (int rc = allreduce_u64(x, &bad, 1, 1)) err = err ? err : rc;
+    else if (bad && !err) err = RTLA_E_COMM;
+  }
+  if (err) {
     rtla_close(x);
-    return RTLA_E_HIP;
+    return err;
   }
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, x->device);
@@ -961,17 +1053,21 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
 
 extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
   if (!x || !buf) return RTLA_E_ARG;
+  std::string fr;  // this process's shards' current levels
+  for (auto& s : x->sh) fr += (fr.empty() ? "" : ", ") + std::to_string(s.n_cur);
   hipDeviceProp_t p;
   HIPCHK(hipGetDeviceProperties(&p, x->device));
   snprintf(buf, cap,
            "{\"device\": \"%s\", \"arch\": \"%s\", \"cus\": %d, \"rank\": %d, \"world\": %d, \"shards\": %d, "
            "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu, "
            "\"transport\": \"%s\", \"sent_cache_slots_log2\": %d, \"rebalanced_rows\": %llu, "
-           "\"sym_key_queue\": %llu, \"sym_round_states\": %llu}",
+           "\"outbox_records_per_owner\": %llu, \"overflow_records\": %llu, \"exchange_rounds\": %llu, "
+           "\"overflowed_records\": %llu, \"shard_frontier\": [%s]}",
            p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
            (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk,
            x->shm ? "shm" : x->comm ? (x->rccl_local ? "rccl-local" : "rccl") : "device", x->nshard > 1 ? x->slog2 : 0,
-           (unsigned long long)x->rebalanced, (unsigned long long)x->qcap, (unsigned long long)x->qchunk);
+           (unsigned long long)x->rebalanced, (unsigned long long)x->box_cap, (unsigned long long)x->over_cap,
+           (unsigned long long)x->rounds, (unsigned long long)x->overflowed, fr.c_str());
   return RTLA_OK;
 }
 
@@ -984,10 +1080,18 @@ static int allreduce2_u64(rtla_ctx* x, uint64_t* sum, int n1, uint64_t* mx, int 
   if (x->world == 1 && !x->rccl_local) return RTLA_OK;
   HIPCHK(hipMemcpyAsync(x->red, sum, 8 * n1, hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipMemcpyAsync(x->red + 32, mx, 8 * n2, hipMemcpyHostToDevice, x->stream));
-  if (!x->shm) NCCLCHK(ncclGroupStart());
-  if (int rc = comm_allreduce(x, x->red, n1, 0)) return rc;
-  if (int rc = comm_allreduce(x, x->red + 32, n2, 1)) return rc;
-  if (!x->shm) NCCLCHK(ncclGroupEnd());
+  if (!x->shm) {  // both reductions in one group (closed also when one could not be posted)
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return nccl_fail(r, __LINE__);
+    r = ncclAllReduce(x->red, x->red, n1, ncclUint64, ncclSum, x->comm, x->stream);
+    if (r == ncclSuccess) r = ncclAllReduce(x->red + 32, x->red + 32, n2, ncclUint64, ncclMax, x->comm, x->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) return nccl_fail(r, __LINE__);
+  } else {
+    if (int rc = comm_allreduce(x, x->red, n1, 0)) return rc;
+    if (int rc = comm_allreduce(x, x->red + 32, n2, 1)) return rc;
+  }
   HIPCHK(hipMemcpyAsync(sum, x->red, 8 * n1, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipMemcpyAsync(mx, x->red + 32, 8 * n2, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
@@ -1244,39 +1348,37 @@ struct Local {
   int flush() { return sends.empty() ? RTLA_OK : comm_exchange(x, sends, recvs); }
 };
 
-// (1) h_out[p] = records this shard queued for owner p, h_in[p] = records
-// owner-shard receives from p; in_count on the device.
+// (1) The round's one synchronisation: every shard's out_count row (records
+// reserved per owner, frontier states left, overflow records) -> x->h_rows
+// on every rank; h_out[p] = records this shard sends owner p, h_in[p] =
+// records it receives from p (reservations past a region's end are on the
+// overflow list: counted up to box_cap); in_count on the device.
 static int gather_counts(rtla_ctx* x) {
-  const int G = x->nshard;
+  const int G = x->nshard, RW = G + 2;
+  x->h_rows.assign((size_t)G * RW, 0);
   if (x->world == 1) {
     for (auto& s : x->sh) {
-      if (x->rccl_local) {  // (one rank: all_count[0, G) = out_count)
-        if (int rc = comm_allgather(x, s.out_count, s.all_count, G)) return rc;
-        HIPCHK(hipMemcpyAsync(s.h_out.data(), s.all_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+      if (x->rccl_local) {  // (one rank: all_count[0, RW) = out_count)
+        if (int rc = comm_allgather(x, s.out_count, s.all_count, RW)) return rc;
+        HIPCHK(hipMemcpyAsync(x->h_rows.data() + (size_t)s.id * RW, s.all_count, 8 * RW, hipMemcpyDeviceToHost,
+                              x->stream));
       } else {
-        HIPCHK(hipMemcpyAsync(s.h_out.data(), s.out_count, 8 * G, hipMemcpyDeviceToHost, x->stream));
+        HIPCHK(hipMemcpyAsync(x->h_rows.data() + (size_t)s.id * RW, s.out_count, 8 * RW, hipMemcpyDeviceToHost,
+                              x->stream));
       }
     }
     HIPCHK(hipStreamSynchronize(x->stream));
-    for (auto& dst : x->sh)
-      for (auto& src : x->sh) dst.h_in[src.id] = src.h_out[dst.id];
   } else {
     Shard& s = x->sh[0];
-    if (int rc = comm_allgather(x, s.out_count, s.all_count, G)) return rc;
-    HIPCHK(hipMemcpyAsync(s.h_all.data(), s.all_count, 8 * G * G, hipMemcpyDeviceToHost, x->stream));
+    if (int rc = comm_allgather(x, s.out_count, s.all_count, RW)) return rc;
+    HIPCHK(hipMemcpyAsync(x->h_rows.data(), s.all_count, 8 * G * RW, hipMemcpyDeviceToHost, x->stream));
     HIPCHK(hipStreamSynchronize(x->stream));
-    for (int p = 0; p < G; p++) {
-      s.h_out[p] = s.h_all[(size_t)s.id * G + p];
-      s.h_in[p] = s.h_all[(size_t)p * G + s.id];
-    }
   }
   for (auto& s : x->sh)
-    for (int p = 0; p < G; p++)
-      if (s.h_out[p] > x->box_cap || s.h_in[p] > x->box_cap) {
-        report_flags(FLAG_OUTBOX_FULL);
-        x->finished = true;
-        return RTLA_E_OVERFLOW;
-      }
+    for (int p = 0; p < G; p++) {
+      s.h_out[p] = std::min(x->h_rows[(size_t)s.id * RW + p], x->box_cap);
+      s.h_in[p] = std::min(x->h_rows[(size_t)p * RW + s.id], x->box_cap);
+    }
   // h_in stays untouched until the next round's synchronisation
   for (auto& s : x->sh) HIPCHK(hipMemcpyAsync(s.in_count, s.h_in.data(), 8 * G, hipMemcpyHostToDevice, x->stream));
   return RTLA_OK;
@@ -1461,33 +1563,24 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
   const Layout& L = x->L;
   const int G = x->nshard;
   std::vector<uint64_t> next_base(x->sh.size()), next_cap(x->sh.size());
+  // capacity shortfalls found here travel in the level's reduction like the kernels' flags
+  // (a rank returning before the collectives would leave the others waiting in them)
+  int lflags = 0;
   for (size_t k = 0; k < x->sh.size(); k++) {
     Shard& s = x->sh[k];
     HIPCHK(hipMemsetAsync(s.ctr, 0, offsetof(DevCounters, cover), x->stream));
     next_base[k] = s.cur_base + s.n_cur;
-    if (next_base[k] >= s.parents_cap) return RTLA_E_OVERFLOW;
-    next_cap[k] = std::min<uint64_t>(next_room(x, s), s.parents_cap - next_base[k]);
+    const bool no_room = next_base[k] >= s.parents_cap;
+    if (no_room) {  // nothing fits: every new state is flagged, none stored
+      lflags |= FLAG_FRONTIER_FULL;
+      next_base[k] = s.parents_cap;
+    }
+    next_cap[k] = no_room ? 0 : std::min<uint64_t>(next_room(x, s), s.parents_cap - next_base[k]);
     s.h_caps[0] = s.n_cur; s.h_caps[1] = next_cap[k]; s.h_caps[2] = s.parents_cap;
     HIPCHK(hipMemcpyAsync(&s.ctr->cap_cur, s.h_caps, sizeof s.h_caps, hipMemcpyHostToDevice, x->stream));
   }
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev0, x->stream));
-  if (G == 1 && x->qcap && !(env_xflags() & XF_WAVE_KERNEL)) {
-    // SYMMETRY: per round, the level kernel evaluates and queues, k_sym_keys
-    // keys, probes and builds the new orbits' rows
-    Shard& s = x->sh[0];
-    ShardBox box{1, 0, (unsigned long long)x->qcap, 0, (unsigned long long*)s.qcount, nullptr,
-                 (unsigned long long*)s.queue};
-    for (uint64_t b = 0; b < s.n_cur; b += x->qchunk) {
-      const uint64_t e = std::min<uint64_t>(b + x->qchunk, s.n_cur);
-      HIPCHK(hipMemsetAsync(s.qcount, 0, 8, x->stream));
-      HIPCHK(launch_expand(L, cur_ring(x, s), b, e, s.cur_base, next_ring(x, s), s.parents, next_base[0],
-                           next_cap[0], s.table, x->tlog2, s.ctr, box, x->grid, x->stream,
-                           env_xflags() | XF_SYM_QUEUE, nullptr, nullptr));
-      HIPCHK(launch_sym_keys(L, cur_ring(x, s), s.cur_base, s.queue, s.qcount, x->qcap, next_ring(x, s), s.parents,
-                             next_base[0], next_cap[0], s.table, x->tlog2, s.ctr, x->stream));
-    }
-    HIPCHK(hipEventRecord(s.evm, x->stream));
-  } else if (G == 1) {
+  if (G == 1) {
     Shard& s = x->sh[0];
     ShardBox box{1, 0, 0, 0, nullptr, nullptr, nullptr};
     uint64_t blocks = (s.n_cur + 3) / 4;
@@ -1496,28 +1589,67 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     HIPCHK(launch_expand(L, cur_ring(x, s), 0, s.n_cur, s.cur_base, next_ring(x, s), s.parents, next_base[0],
                          next_cap[0], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), nullptr, s.evm));
   } else {
-    // lock-step chunks over the frontier; every shard runs the same number
-    // (x->max_front = the largest frontier of any shard, from the last level's reduction)
-    const uint64_t rounds = std::max<uint64_t>(1, (x->max_front + x->chunk - 1) / x->chunk);
-    for (uint64_t c = 0; c < rounds; c++) {
+    // Exchange rounds.  Each round every shard requeues its overflow list,
+    // expands the rest of its frontier until an owner region of its outbox
+    // fills (or, without the group guard, x->chunk states), and the records
+    // travel (gather_counts .. k_build_winners).  Every rank learns from the
+    // round's count gather what every shard has left, so all issue the same
+    // collectives, and the rounds end together once nothing is left.
+    for (auto& s : x->sh) {
+      s.pos = 0;
+      s.over_n = 0;
+    }
+    uint64_t last_left = ~0ull;
+    for (uint64_t round = 0;; round++) {
       for (size_t k = 0; k < x->sh.size(); k++) {
         Shard& s = x->sh[k];
-        uint64_t b = std::min<uint64_t>(c * x->chunk, s.n_cur), e = std::min<uint64_t>(b + x->chunk, s.n_cur);
+        const int nv = s.ov ^ 1;  // the overflow list this round appends to
         HIPCHK(hipMemsetAsync(s.out_count, 0, 8 * G, x->stream));
+        HIPCHK(hipMemsetAsync(s.over_cnt + nv, 0, 8, x->stream));
         ShardBox box{G, s.id, (unsigned long long)x->box_cap, x->slog2, (unsigned long long*)s.out_count,
-                     (unsigned long long*)s.send_fp, (unsigned long long*)s.send_ref};
-        uint64_t blocks = (e - b + 3) / 4;
-        int grid = (int)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), (uint64_t)x->grid);
-        HIPCHK(launch_expand(L, cur_ring(x, s), b, e, s.cur_base, next_ring(x, s), s.parents, next_base[k],
-                             next_cap[k], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), s.sent));
+                     (unsigned long long*)s.send_fp, (unsigned long long*)s.send_ref,
+                     (unsigned long long)x->stop_at, (unsigned long long*)s.over_fp[nv],
+                     (unsigned long long*)s.over_ref[nv], (unsigned long long*)(s.over_cnt + nv),
+                     (unsigned long long)x->over_cap};
+        HIPCHK(launch_requeue(s.over_fp[s.ov], s.over_ref[s.ov], s.over_cnt + s.ov, s.over_n, box, s.ctr, x->stream));
+        const uint64_t b = s.pos, e = x->chunk ? std::min<uint64_t>(s.n_cur, b + x->chunk) : s.n_cur;
+        if (e > b) {
+          uint64_t blocks = (e - b + 3) / 4;
+          int grid = (int)std::min<uint64_t>(std::max<uint64_t>(blocks, 1), (uint64_t)x->grid);
+          HIPCHK(launch_expand(L, cur_ring(x, s), b, e, s.cur_base, next_ring(x, s), s.parents, next_base[k],
+                               next_cap[k], s.table, x->tlog2, s.ctr, box, grid, x->stream, env_xflags(), s.sent));
+        }
+        HIPCHK(launch_round_tail(s.ctr, s.out_count, G, e - b, s.n_cur - e, x->guarded && e > b, s.over_cnt + nv,
+                                 x->stream));
+        s.ov = nv;
       }
+      if (round == 0 && fault_here(x, "exchange")) lflags |= FLAG_LOCAL_FAILURE;
       int rc = gather_counts(x);
       if (rc) return rc;
+      const int RW = G + 2;
+      uint64_t left = 0, sent_recs = 0;  // frontier states and overflow records left anywhere, records this round
+      for (int r = 0; r < G; r++) {
+        left += x->h_rows[(size_t)r * RW + G] + x->h_rows[(size_t)r * RW + G + 1];
+        for (int p = 0; p < G; p++) sent_recs += x->h_rows[(size_t)r * RW + p];
+      }
+      for (auto& s : x->sh) {
+        s.pos = s.n_cur - x->h_rows[(size_t)s.id * RW + G];
+        s.over_n = x->h_rows[(size_t)s.id * RW + G + 1];
+        x->overflowed += s.over_n;
+      }
+      x->rounds++;
+      if (left && !sent_recs && left >= last_left) {  // (cannot happen: a round with room takes a group)
+        fprintf(stderr, "rtla: exchange round %llu made no progress\n", (unsigned long long)round);
+        report_flags(FLAG_OUTBOX_FULL);
+        x->finished = true;
+        return RTLA_E_OVERFLOW;
+      }
+      last_left = left;
       rc = move_fps(x);
       if (rc) return rc;
       for (auto& s : x->sh) {
         uint64_t mx_in = 0;
-        for (uint64_t v : s.h_in) mx_in = std::max(mx_in, v);
+        for (int p = 0; p < G; p++) mx_in = std::max(mx_in, s.h_in[p]);
         HIPCHK(launch_insert_remote(s.recv_fp, s.in_count, G, x->box_cap, s.table, x->tlog2, s.recv_ans, s.ctr, mx_in,
                                     x->stream));
       }
@@ -1526,16 +1658,20 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
       for (size_t k = 0; k < x->sh.size(); k++) {  // each sender builds its winners into its own next level
         Shard& s = x->sh[k];
         uint64_t mx_out = 0;
-        for (uint64_t v : s.h_out) mx_out = std::max(mx_out, v);
+        for (int p = 0; p < G; p++) mx_out = std::max(mx_out, s.h_out[p]);
         HIPCHK(launch_build_winners(L, cur_ring(x, s), s.cur_base, s.id, s.send_ref, s.send_ans, s.out_count, G,
                                     x->box_cap, next_ring(x, s), s.parents, next_base[k], next_cap[k], s.ctr, mx_out,
                                     x->stream));
       }
+      if (!left) break;
     }
   }
   for (auto& s : x->sh) HIPCHK(hipEventRecord(s.ev1, x->stream));
   // gather counters
-  uint64_t sums[4 + SHARD_MAX] = {};  // new, generated, probes, frontier, next-level states per shard (global id)
+  // new, generated, probes, frontier, next-level states per shard (global id), then one count per flag bit
+  // (bits are summed, not max-reduced: every rank then reports the union of the flags)
+  constexpr int NFLAG = 8;
+  uint64_t sums[4 + SHARD_MAX + NFLAG] = {};
   uint64_t maxs[4] = {0, 0, 0, 0};  // flags, violation, device time (us), largest next frontier of a shard
   double emax = 0.0;  // probe-kernel (k_expand_*) time of this level, ms
   std::vector<DevCounters> hc(x->sh.size());
@@ -1551,7 +1687,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     emax = std::max(emax, (double)ems);
     sums[0] += hc[k].next_count; sums[1] += hc[k].generated; sums[2] += hc[k].probes; sums[3] += s.n_cur;
     sums[4 + s.id] = hc[k].next_count;
-    maxs[0] |= (uint64_t)hc[k].flags;
+    lflags |= hc[k].flags;
     maxs[1] = std::max<uint64_t>(maxs[1], hc[k].viol_mask ? 1 : 0);
     maxs[2] = std::max<uint64_t>(maxs[2], (uint64_t)(kms * 1000.0));
     maxs[3] = std::max<uint64_t>(maxs[3], hc[k].next_count);
@@ -1561,8 +1697,12 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
     }
   }
   print_stamps(hc[0], x->level + 1);
-  int rc = allreduce2_u64(x, sums, 4 + (G > 1 ? G : 0), maxs, 4);
+  const int nsum = 4 + (G > 1 ? G : 0);
+  for (int b = 0; b < NFLAG; b++) sums[nsum + b] = (uint64_t)(lflags >> b & 1);
+  int rc = allreduce2_u64(x, sums, nsum + NFLAG, maxs, 4);
   if (rc) return rc;
+  for (int b = 0; b < NFLAG; b++)
+    if (sums[nsum + b]) maxs[0] |= 1ull << b;
   x->max_front = maxs[3];
   if (maxs[0]) {
     report_flags((int)maxs[0]);
@@ -1703,17 +1843,24 @@ extern "C" int rtla_level_orbit_hash(rtla_ctx* x, int threads, uint64_t* out) {
   return level_digest(x, threads, out, true);
 }
 
+// Collective when world > 1: a local failure (device, read-back) travels in
+// the reduction (its last word), so every rank fails together.
 extern "C" int rtla_coverage(rtla_ctx* x, uint64_t* gen, uint64_t* distinct, int n) {
   if (!x) return RTLA_E_ARG;
-  HIPCHK(hipSetDevice(x->device));
-  std::vector<uint64_t> acc(2 * COVER_CODES, 0);
+  std::vector<uint64_t> acc(2 * COVER_CODES + 1, 0);
+  bool bad = hipSetDevice(x->device) != hipSuccess || fault_here(x, "coverage");
   for (auto& s : x->sh) {
     DevCounters h;
-    HIPCHK(hipMemcpy(&h, s.ctr, sizeof h, hipMemcpyDeviceToHost));
+    if (bad || hipMemcpy(&h, s.ctr, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) {
+      bad = true;
+      break;
+    }
     for (int k = 0; k < 2 * COVER_CODES; k++) acc[k] += h.cover[k];
   }
-  int rc = allreduce_u64(x, acc.data(), 2 * COVER_CODES, 0);
+  acc[2 * COVER_CODES] = bad ? 1 : 0;
+  int rc = allreduce_u64(x, acc.data(), 2 * COVER_CODES + 1, 0);
   if (rc) return rc;
+  if (acc[2 * COVER_CODES]) return bad ? RTLA_E_HIP : RTLA_E_COMM;
   for (int k = 0; k < n && k < COVER_CODES; k++) {
     if (gen) gen[k] = acc[k];
     if (distinct) distinct[k] = acc[COVER_CODES + k];
@@ -1729,7 +1876,10 @@ extern "C" int rtla_coverage(rtla_ctx* x, uint64_t* gen, uint64_t* distinct, int
 // each step's record is broadcast by the rank that holds it).
 extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t cap, size_t* n_rows) {
   if (!x || !n_rows) return RTLA_E_ARG;
-  HIPCHK(hipSetDevice(x->device));
+  // world > 1: every rank reaches every reduction below; a local failure
+  // travels in them (a failure count), so all ranks stop at the same step
+  bool bad = hipSetDevice(x->device) != hipSuccess || fault_here(x, "trace");
+  if (bad && x->world == 1) return RTLA_E_HIP;
   const Layout& L = x->L;
   // start: (holder shard, shard-local index, pending instance or -1)
   uint64_t start[4] = {0, 0, 0, 0};  // has, shard, g, inst + 1
@@ -1745,16 +1895,17 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
   }
   if (x->world > 1) {
     // the lowest shard holding a violation publishes its start record
-    uint64_t holder = start[0] ? start[1] : (uint64_t)x->nshard;
-    uint64_t mn = (uint64_t)x->nshard - holder;  // max of (G - holder) == min holder
-    int rc = allreduce_u64(x, &mn, 1, 1);
+    uint64_t v[2] = {(uint64_t)x->nshard - (start[0] ? start[1] : (uint64_t)x->nshard), bad ? 1ull : 0ull};
+    int rc = allreduce_u64(x, v, 2, 1);  // max of (G - holder) == min holder; any failure
     if (rc) return rc;
-    if (mn == 0) return RTLA_E_STATE;
-    int root = (int)((uint64_t)x->nshard - mn);
-    HIPCHK(hipMemcpyAsync(x->red, start, 32, hipMemcpyHostToDevice, x->stream));
-    if (int rc2 = comm_bcast(x, x->red, 4, root)) return rc2;
-    HIPCHK(hipMemcpyAsync(start, x->red, 32, hipMemcpyDeviceToHost, x->stream));
-    HIPCHK(hipStreamSynchronize(x->stream));
+    if (v[1]) return bad ? RTLA_E_HIP : RTLA_E_COMM;
+    if (v[0] == 0) return RTLA_E_STATE;
+    const int root = (int)((uint64_t)x->nshard - v[0]);
+    uint64_t w[5] = {0, 0, 0, 0, 0};  // root's start record, then the failure count
+    if (x->rank == root) memcpy(w, start, 32);
+    rc = allreduce_u64(x, w, 5, 0);
+    if (rc) return rc;
+    memcpy(start, w, 32);
   } else if (!start[0]) {
     return RTLA_E_STATE;
   }
@@ -1771,10 +1922,15 @@ extern "C" int rtla_trace(rtla_ctx* x, uint32_t* rows, int32_t* labels, size_t c
       HIPCHK(hipMemcpyAsync(&p, x->red, 8, hipMemcpyDeviceToHost, x->stream));
       HIPCHK(hipStreamSynchronize(x->stream));
     } else {
-      if ((int)shard == x->rank) HIPCHK(hipMemcpyAsync(x->red, x->sh[0].parents + g, 8, hipMemcpyDeviceToDevice, x->stream));
-      if (int rc2 = comm_bcast(x, x->red, 1, (int)shard)) return rc2;
-      HIPCHK(hipMemcpyAsync(&p, x->red, 8, hipMemcpyDeviceToHost, x->stream));
-      HIPCHK(hipStreamSynchronize(x->stream));
+      // the holder contributes the record, every rank its failure flag
+      uint64_t w[2] = {0, 0};
+      if ((int)shard == x->rank && !bad && hipMemcpy(&w[0], x->sh[0].parents + g, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        bad = true;
+      w[1] = bad ? 1 : 0;
+      if ((int)shard == x->rank && bad) w[0] = 0;
+      if (int rc2 = allreduce_u64(x, w, 2, 0)) return rc2;
+      if (w[1]) return bad ? RTLA_E_HIP : RTLA_E_COMM;
+      p = w[0];
     }
     if (p == ~0ull) break;  // Init
     insts.push_back((int32_t)(p & 0xffff));

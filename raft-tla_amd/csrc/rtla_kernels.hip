@@ -56,6 +56,71 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
   if (lane == 0 && probes) atomicAdd(&ctr->probes, (unsigned long long)probes);
 }
 
+// Exchange round start: the previous round's overflow list (records queued
+// past their owner region's end) into this round's outbox regions -- the
+// regions are empty, so nearly all fit; what does not goes back on the new
+// overflow list.  One record per lane; a wave reserves each owner's slots
+// with one atomic.
+__global__ void k_requeue(const unsigned long long* __restrict__ in_fp, const unsigned long long* __restrict__ in_ref,
+                          const unsigned long long* __restrict__ in_count, ShardBox box, DevCounters* ctr) {
+  const unsigned long long n = *in_count;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanes_below = (1ull << lane) - 1ull;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  const unsigned long long start = (unsigned long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  for (unsigned long long k0 = start; k0 < n; k0 += stride) {  // (wave-uniform trip count)
+    const unsigned long long k = k0 + lane;
+    const bool act = k < min(n, box.over_cap);
+    const FP f = act ? FP{in_fp[2 * k], in_fp[2 * k + 1]} : FP{0, 0};
+    const unsigned long long ref = act ? in_ref[k] : 0ull;
+    const int o = act ? fp_owner(f, box.nshard) : -1;
+    unsigned long long slot = ~0ull;
+    for (int p = 0; p < box.nshard; p++) {
+      const unsigned long long m = __ballot(o == p);
+      if (!m) continue;
+      unsigned long long b = 0;
+      if (lane == __builtin_ctzll(m)) b = atomicAdd(&box.out_count[p], (unsigned long long)__popcll(m));
+      b = shfl_u64(b, __builtin_ctzll(m));
+      if (o == p) slot = b + __popcll(m & lanes_below);
+    }
+    if (act && slot < box.cap) {
+      const unsigned long long q = (unsigned long long)o * box.cap + slot;
+      box.send_fp[2 * q] = f.a;
+      box.send_fp[2 * q + 1] = f.b;
+      box.send_ref[q] = ref;
+    }
+    const bool ov = act && slot >= box.cap;
+    const unsigned long long om = __ballot(ov);
+    if (om) {
+      unsigned long long ob = 0;
+      if (lane == 0) ob = atomicAdd(box.over_count, (unsigned long long)__popcll(om));
+      ob = shfl0_u64(ob);
+      if (ov) {
+        const unsigned long long q = ob + __popcll(om & lanes_below);
+        if (q < box.over_cap) {
+          box.over_fp[2 * q] = f.a;
+          box.over_fp[2 * q + 1] = f.b;
+          box.over_ref[q] = ref;
+        } else {
+          set_flag(ctr, FLAG_OUTBOX_FULL);
+        }
+      }
+    }
+  }
+}
+
+// Exchange round end, on the device (read back by the round's one count
+// gather): how much of the frontier range the level kernel left, and the
+// overflow list's length.
+__global__ void k_round_tail(const DevCounters* ctr, unsigned long long* out, int G, unsigned long long span,
+                             unsigned long long rest, int grouped, const unsigned long long* over_count) {
+  if (threadIdx.x != 0) return;
+  unsigned long long done = span;
+  if (grouped) done = min(span, ctr->group_next * ctr->group_size);
+  out[G] = rest + span - done;
+  out[G + 1] = over_count ? *over_count : 0ull;
+}
+
 // Re-balancing, receiving side: append the staged rows to the next frontier
 // (one wave per row, coalesced copy) with their parent records.
 __global__ void k_unpack_rows(int W, const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ counts,
@@ -209,7 +274,7 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
                          uint64_t* sent, hipEvent_t mid) {
   if (s_end <= s_begin) return hipSuccess;
   const int cwpb = expand_compact_wpb(L);
-  if (cwpb > 0 && !(xflags & XF_WAVE_KERNEL) && (box.nshard == 1 || sent)) {
+  if (cwpb > 0 && !(xflags & XF_WAVE_KERNEL)) {
     const CompactArgs a{L,         box.nshard > 1, cur,      s_begin, s_end,  cur_base, next,   parents, next_base,
                         next_cap,  table,          tlog2,    ctr,     box,    st,       xflags, sent,
                         (xflags & XF_BLOCK4) ? cwpb : 1};  // one-wave workgroups by default
@@ -238,6 +303,53 @@ hipError_t launch_expand(const Layout& L, const Ring& cur, uint64_t s_begin, uin
   // (or forced, XF_WAVE_KERNEL)
   return launch_wave_expand(L, cur, s_begin, s_end, cur_base, next, parents, next_base, next_cap, table, tlog2, ctr,
                             box, grid, st);
+}
+
+bool level_kernel_shape(const Layout& L, bool multi, int xflags, int* waves, int* group) {
+  *waves = 0;
+  *group = 0;
+  if (expand_compact_wpb(L) <= 0 || (xflags & XF_WAVE_KERNEL)) return false;
+  int q[2] = {0, 0};
+  CompactArgs a{};
+  a.L = L;
+  a.multi = multi;
+  a.s_begin = 0;
+  a.s_end = 64;
+  a.xflags = xflags;
+  a.wpb = (xflags & XF_BLOCK4) ? expand_compact_wpb(L) : 1;
+  a.box.nshard = multi ? 2 : 1;
+  a.query = q;
+  bool done = false;
+  if (!(xflags & XF_NO_SPECIAL)) {
+    (void)launch_compact_spec_a(a, &done);
+    if (!done) (void)launch_compact_spec_b(a, &done);
+  }
+#ifndef RTLA_EXP_MINIMAL
+  if (!done && L.sym) (void)launch_compact_sym_a(a, &done);
+  if (!done && L.sym) (void)launch_compact_sym_b(a, &done);
+  if (!done) (void)launch_compact_generic_a(a, &done);
+  if (!done) (void)launch_compact_generic_b(a, &done);
+#endif
+  if (!done || q[0] <= 0 || q[1] <= 0) return false;
+  *waves = q[0];
+  *group = q[1];
+  return true;
+}
+
+hipError_t launch_requeue(const uint64_t* in_fp, const uint64_t* in_ref, const uint64_t* in_count, uint64_t max_count,
+                          const ShardBox& box, DevCounters* ctr, hipStream_t st) {
+  if (!max_count) return hipSuccess;
+  hipLaunchKernelGGL(k_requeue, dim3(grid_x(max_count, 256)), dim3(256), 0, st, (const unsigned long long*)in_fp,
+                     (const unsigned long long*)in_ref, (const unsigned long long*)in_count, box, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_round_tail(const DevCounters* ctr, uint64_t* out, int G, uint64_t span, uint64_t rest, bool grouped,
+                             const uint64_t* over_count, hipStream_t st) {
+  hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(64), 0, st, ctr, (unsigned long long*)out, G,
+                     (unsigned long long)span, (unsigned long long)rest, grouped ? 1 : 0,
+                     (const unsigned long long*)over_count);
+  return hipGetLastError();
 }
 
 hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts, int nshard, uint64_t cap,

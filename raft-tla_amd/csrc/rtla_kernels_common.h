@@ -356,7 +356,6 @@ constexpr int NEWCAP = 512; // new-state list (u16: state lane << 8 | instance)
 // entries before the flush.
 constexpr int NEWFLUSH = NEWCAP - 3 * 64;
 
-constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a time (MULTI)
 
 // Per-wave LDS of k_expand_compact (16-byte aligned pieces first):
 // per-state fingerprint with allLogs' applied (GROUP FPs) | SYMMETRY: the
@@ -366,19 +365,9 @@ constexpr int OBOX_CHUNK = 256;  // outbox slots a wave reserves per owner at a 
 // key continuations (64 least-image-so-far FPs, 64 entries).
 // (The outbox state exists only in the MULTI kernels: one shard's tile then
 // stays small enough for 12 one-wave blocks per CU on configs[1]'s 372-byte rows.)
-// RTLA_CHILD_STAGE > 0: child rows are built in an LDS stage of that many
-// rows (patched there, stored once).  Measured on configs[1]: HBM writes
-// 13.2 -> 10.0 GB per launch (1.09x the rows + CAS), but 197 -> 220 / 232 /
-// 286 ms per step at 16 / 32 / 64 rows (the patches run once per stage, and
-// the stage costs waves) -- so 0: copy the parent rows to HBM, then patch
-// the differing words there.
-#ifndef RTLA_CHILD_STAGE
-#define RTLA_CHILD_STAGE 0
-#endif
-constexpr int CSTAGE = RTLA_CHILD_STAGE;
 __host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym, bool multi) {
   return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW +
-          RING / 2 * (sym ? 2 : 1) + (sym ? 5 * 64 : 0) + CSTAGE * W + 3) & ~3;
+          RING / 2 * (sym ? 2 : 1) + (sym ? 5 * 64 : 0) + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -435,6 +424,11 @@ __device__ __forceinline__ void outbox_holes(const ShardBox& box, int o, unsigne
     box.send_fp[2 * k] = 0ull;
     box.send_fp[2 * k + 1] = 0ull;
   }
+}
+
+// Home slot of a key in a table of 2^lg slots (lg = 0: no table, slot 0).
+__device__ __forceinline__ unsigned long long home_slot(const FP& key, int lg) {
+  return lg ? key.a >> (64 - lg) : 0ull;
 }
 
 __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
@@ -572,9 +566,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // queued by the evaluation pass and keyed 64 at a time (key_chunk)
   uint16_t* kring = ring + RING;
   int kpos = 0, kdone = 0;
-  // XF_SYM_QUEUE: this wave's open chunk of the HBM key queue (wave-uniform)
-  unsigned long long qb = ~0ull;
-  int qu = OBOX_CHUNK;
   // SYMMETRY: successors whose orbit key needs more images than key_chunk
   // computes per pass (one): entry (state lane << 8 | instance | next image
   // << 16) and the least image fingerprint so far; taken first by the next
@@ -582,7 +573,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   FP* cbest = reinterpret_cast<FP*>(kring + (SYM ? RING : 0));
   uint32_t* cent = reinterpret_cast<uint32_t*>(cbest + (SYM ? 64 : 0));
   int ccount = 0;
-  uint32_t* cstage = cent + (SYM ? 64 : 0);  // CSTAGE child rows
   if (MULTI) {
     if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
@@ -679,7 +669,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         while (w >= W) { w -= W; r++; }
       }
     };
-    if (CSTAGE == 0 && rows_on) copy_rows(0, nrows);  // (all of them first: one pass of coalesced stores)
+    if (rows_on) copy_rows(0, nrows);  // (all of them first: one pass of coalesced stores)
     for (int b = 0; b < ntot; b += 64) {  // (2), (3)
       const bool act = b + lane < ntot;
       const int e = act ? newl[(head + b + lane) & (NEWCAP - 1)] : 0;
@@ -715,37 +705,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       }
       uint32_t spk[PACKW], epk[PACKW];  // the changed records, packed
       if (act) child_pack(L, d, spk, epk);
-      if (CSTAGE > 0 && rows_on) {
-        // (1) + (3) in LDS, CSTAGE children at a time: the parent rows are
-        // copied into the stage, each child's lane patches the words in
-        // which it differs, and the wave stores the finished rows once,
-        // coalesced (no second write of any HBM line)
-        const int bn = min(64, nrows - b);
-        for (int c0 = 0; c0 < bn; c0 += CSTAGE) {
-          const int cn = min(CSTAGE, bn - c0);
-          for (int t = lane; t < cn * W; t += 64) {
-            const int r = t / W;
-            const int sr = newl[(head + b + c0 + r) & (NEWCAP - 1)] >> 8;
-            cstage[t] = rows[sr * W + (t - r * W)];
-          }
-          wave_sync();
-          if (lane >= c0 && lane < c0 + cn) {
-            const StridedWords<GROUP> pall_p{pall + sl};
-            uint32_t* dst = cstage + (lane - c0) * W;
-            child_write(L, rows + sl * W, d, spk, epk, pall_p, cfp, [&](int w, uint32_t v) { dst[w] = v; });
-          }
-          wave_sync();
-          const int off0 = (b + c0) * W;
-          for (int t = lane; t < cn * W; t += 64) {
-            const int i = off0 + t;
-            const uint32_t v = cstage[t];
-            if (i < n1) d1[i] = v;
-            else next.base[i - n1] = v;
-          }
-          wave_sync();  // (the stage is refilled next)
-        }
-      }
-      if (CSTAGE == 0 && rows_on) {  // (3): the copies must land first (same words, other lanes)
+      if (rows_on) {  // (3): the copies must land first (same words, other lanes)
         if (b == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (child < nrows) {
           const StridedWords<GROUP> pall_p{pall + sl};
@@ -772,7 +732,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 #endif
     if (cpend) {
       if (MULTI && cowner != me) {  // the sent cache: overwrite, report "not sent before"
-        sent[cidx] = ckey;
+        if (box.slog2) sent[cidx] = ckey;
         cold = 0ull;
       } else {
         cold = atomicCAS(&table[cidx], 0ull, ckey);
@@ -803,7 +763,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       if (pend) {  // this chunk's load -> seen, or a CAS (sent cache: a store) for the next issue
         const bool to_sent = MULTI && powner != me;
         const int lg = to_sent ? box.slog2 : tlog2;
-        const unsigned long long key = pf.b | 1ull, idx = pf.a >> (64 - lg);
+        const unsigned long long key = pf.b | 1ull, idx = home_slot(pf, lg);
         if (pold != key) {
           cidx = (to_sent || pold == 0ull) ? idx : ((idx + 1ull) & ((1ull << lg) - 1ull));
           ckey = key;
@@ -818,59 +778,77 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     } else if (pend) {
       if (MULTI && powner != me) {  // the sent cache: a miss overwrites the slot
         isnew = pold != (pf.b | 1ull);
-        if (isnew) sent[pf.a >> (64 - box.slog2)] = pf.b | 1ull;
+        if (isnew && box.slog2) sent[home_slot(pf, box.slog2)] = pf.b | 1ull;
       } else {
         const unsigned long long pidx = pf.a >> (64 - tlog2);
         isnew = (xflags & XF_CAS_ONLY) ? fpset_resolve(table, tlog2, pf.b | 1ull, pidx, pold, ctr)
                                        : fpset_resolve_loaded(table, tlog2, pf.b | 1ull, pidx, pold, ctr);
       }
     }
-    if (MULTI) {  // records for other owners: one outbox reservation per (wave, owner)
+    if (MULTI) {  // records for other owners: all owners' outbox slots reserved in one step
       const int powner = nowner_r;
       const FP pf = nf;
-      const unsigned long long prec =
-          (unsigned long long)me << 56 | (cur_base + s0 + (ninfo >> 16)) << 16 | (unsigned long long)(ninfo & 0xffffu);
       const bool rem = isnew && powner != me;
       isnew = isnew && powner == me;
-      // owners with records this chunk: a ballot per owner for few shards (a
-      // wave-wide OR is a chain of 6 cross-lane exchanges per resolve)
-      unsigned long long om = 0;
-      if (box.nshard <= 8) {
-        for (int o = 0; o < box.nshard; o++)
-          if (__ballot(rem && powner == o)) om |= 1ull << o;
-      } else {
-        om = wave_or_u64(rem ? 1ull << powner : 0ull);
-      }
-      while (om) {
-        const int o = __builtin_ctzll(om);
-        om &= om - 1;
-        const unsigned long long m = __ballot(rem && powner == o);
-        const int cnt = __popcll(m);
-        unsigned long long b = obox[o], used = obox[SHARD_MAX + o];
-        if (used + cnt > OBOX_CHUNK) {  // close the open chunk (holes = zero records), reserve the next
-          if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
-          unsigned long long nb = 0;
-          if (lane == 0) nb = atomicAdd(&box.out_count[o], (unsigned long long)OBOX_CHUNK);
-          b = shfl0_u64(nb);
-          used = 0;
+      if (__ballot(rem)) {
+        // lane o learns how many records owner o gets (ocnt), each record its
+        // rank among its owner's (r)
+        unsigned long long mym = 0;
+        int ocnt = 0;
+        for (int o = 0; o < box.nshard; o++) {
+          const unsigned long long m = __ballot(rem && powner == o);
+          if (powner == o) mym = m;
+          if (lane == o) ocnt = __popcll(m);
         }
-        if (rem && powner == o) {
-          const unsigned long long slot = b + used + __popcll(m & lanes_below);
-          if (slot < box.cap) {
-            const unsigned long long k = (unsigned long long)o * box.cap + slot;
-            box.send_fp[2 * k] = pf.a;
-            box.send_fp[2 * k + 1] = pf.b;
-            box.send_ref[k] = (((prec >> 16) & ((1ull << 40) - 1ull)) - cur_base) << 16 | (prec & 0xffffull);
+        // lane o keeps owner o's open chunk of OBOX_CHUNK slots (obox[o] =
+        // its base, obox[SHARD_MAX + o] = slots used); a run that does not fit
+        // continues in a fresh chunk (one atomic per OBOX_CHUNK records, no holes)
+        unsigned long long b1 = 0, b2 = 0;
+        int room = 0;
+        if (ocnt > 0) {
+          const unsigned long long b = obox[lane], used = obox[SHARD_MAX + lane];
+          room = b == ~0ull ? 0 : (int)(OBOX_CHUNK - used);
+          b1 = b + used;
+          if (ocnt > room) {
+            b2 = atomicAdd(&box.out_count[lane], (unsigned long long)OBOX_CHUNK);
+            obox[lane] = b2;
+            obox[SHARD_MAX + lane] = (unsigned long long)(ocnt - room);
           } else {
-            set_flag(ctr, FLAG_OUTBOX_FULL);
+            obox[SHARD_MAX + lane] = used + (unsigned long long)ocnt;
           }
         }
-        wave_sync();
-        if (lane == 0) {
-          obox[o] = b;
-          obox[SHARD_MAX + o] = used + cnt;
+        const int src = rem ? powner : 0;
+        b1 = shfl_u64(b1, src);
+        b2 = shfl_u64(b2, src);
+        room = __shfl(room, src);
+        const int r = __popcll(mym & lanes_below);
+        const unsigned long long slot = r < room ? b1 + r : b2 + (r - room);
+        const unsigned long long ref = (s0 + (ninfo >> 16)) << 16 | (unsigned long long)(ninfo & 0xffffu);
+        if (rem && slot < box.cap) {
+          const unsigned long long k = (unsigned long long)powner * box.cap + slot;
+          box.send_fp[2 * k] = pf.a;
+          box.send_fp[2 * k + 1] = pf.b;
+          box.send_ref[k] = ref;
         }
-        wave_sync();
+        // past the region's end (the groups in flight when it filled): the
+        // overflow list, sent next round
+        const bool ov = rem && slot >= box.cap;
+        const unsigned long long om = __ballot(ov);
+        if (om) {
+          unsigned long long ob = 0;
+          if (lane == 0) ob = atomicAdd(box.over_count, (unsigned long long)__popcll(om));
+          ob = shfl0_u64(ob);
+          if (ov) {
+            const unsigned long long k = ob + __popcll(om & lanes_below);
+            if (k < box.over_cap) {
+              box.over_fp[2 * k] = pf.a;
+              box.over_fp[2 * k + 1] = pf.b;
+              box.over_ref[k] = ref;
+            } else {
+              set_flag(ctr, FLAG_OUTBOX_FULL);
+            }
+          }
+        }
       }
     }
     const unsigned long long m = __ballot(isnew);
@@ -954,34 +932,14 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           nprobe = !(xflags & XF_NO_PROBE);
           ncf = key;
           nowner = MULTI ? fp_owner(key, box.nshard) : me;
-          nidx = key.a >> (64 - ((MULTI && nowner != me) ? box.slog2 : tlog2));
+          nidx = home_slot(key, (MULTI && nowner != me) ? box.slog2 : tlog2);
         }
       }
     }
     if constexpr (KSPLIT) {
       const unsigned long long km = __ballot(kq);
-      if (xflags & XF_SYM_QUEUE) {  // to the HBM queue, for k_sym_keys
-        if (km) {
-          const int cnt = __popcll(km);
-          if (qu + cnt > OBOX_CHUNK) {  // close the open chunk (holes = ~0), reserve the next
-            if (qb != ~0ull)
-              for (unsigned long long j = qb + qu + lane; j < min(qb + OBOX_CHUNK, box.cap); j += 64) box.send_ref[j] = ~0ull;
-            unsigned long long nb = 0;
-            if (lane == 0) nb = atomicAdd(box.out_count, (unsigned long long)OBOX_CHUNK);
-            qb = shfl0_u64(nb);
-            qu = 0;
-          }
-          if (kq) {
-            const unsigned long long slot = qb + qu + __popcll(km & lanes_below);
-            if (slot < box.cap) box.send_ref[slot] = (s0 + sl) << 16 | (unsigned long long)inst;
-            else set_flag(ctr, FLAG_OUTBOX_FULL);
-          }
-          qu += cnt;
-        }
-      } else {
-        if (kq) kring[(kpos + __popcll(km & lanes_below)) & (RING - 1)] = (uint16_t)(sl << 8 | inst);
-        kpos += __popcll(km);
-      }
+      if (kq) kring[(kpos + __popcll(km & lanes_below)) & (RING - 1)] = (uint16_t)(sl << 8 | inst);
+      kpos += __popcll(km);
     }
     if (!(xflags & XF_NO_COVER)) {  // generated coverage, aggregated over equal codes
       const int code = en ? cover_code(L, inst, d.sub) : -1;
@@ -1046,7 +1004,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         nprobe = !(xflags & XF_NO_PROBE);
         ncf = key;
         nowner = MULTI ? fp_owner(key, box.nshard) : me;
-        nidx = key.a >> (64 - ((MULTI && nowner != me) ? box.slog2 : tlog2));
+        nidx = home_slot(key, (MULTI && nowner != me) ? box.slog2 : tlog2);
       }
     }
     const unsigned long long cm = __ballot(next >= 0);
@@ -1071,7 +1029,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       // load first: most successors are already in the set, and a plain
       // load is cheaper than an atomic at the memory side; the CAS is
       // only issued (at resolve time) when the home slot reads empty
-      if (!(xflags & XF_ALL_SUCCESSORS))
+      if (MULTI && nowner != me && !box.slog2)
+        pold = 0ull;  // no sent cache: every remote successor is queued for its owner
+      else if (!(xflags & XF_ALL_SUCCESSORS))
         pold = ((xflags & XF_CAS_ONLY) && !(MULTI && nowner != me))
                    ? atomicCAS(slotp, 0ull, ncf.b | 1ull)
                    : __hip_atomic_load(slotp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1113,11 +1073,26 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   // no static partition, no tail.  (The occupancy API can over-report the
   // resident blocks by one per CU; a static stride would then serialise 1/k
   // of the work behind the rest.)
+  // MULTI: a wave takes its next group at the end of the current one, and
+  // only while no owner region of the outbox has reached box.stop_at; the
+  // groups taken are always a prefix [0, group_next) of the range, so the
+  // driver continues the level from there in the next exchange round.  At
+  // most two groups per wave run after a region fills (the overflow list's
+  // capacity covers them).
+  auto take_group = [&]() -> unsigned long long {
+    const bool full = MULTI && lane < box.nshard && lane != me &&
+                      __hip_atomic_load(&box.out_count[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= box.stop_at;
+    unsigned long long g = ~0ull;
+    if (!__ballot(full) && lane == 0) g = atomicAdd(&ctr->group_next, 1ull);
+    return g;
+  };
+  if (blockIdx.x == 0 && lane == 0 && wave == 0) ctr->group_size = GROUP;
   unsigned long long gnext = 0;
-  if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
+  if (MULTI) gnext = take_group();
+  else if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
   const unsigned long long ngroups = (s_end - s_begin + GROUP - 1) / GROUP;
   for (unsigned long long gi = shfl0_u64(gnext); gi < ngroups; gi = shfl0_u64(gnext)) {
-    if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
+    if (!MULTI && lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);
     s0 = s_begin + gi * GROUP;
     const int nvalid = (int)min<unsigned long long>((unsigned long long)GROUP, s_end - s0);
     {  // s0 and cur.start are multiples of GROUP: the group's rows are contiguous in the arena
@@ -1127,8 +1102,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       if (RTLA_IDX_OK(ctr, ring_idx(cur, s0) + nvalid, cur.cap + 1)) copy_words_lds16(rows, src, nw, lane);
     }
     wave_sync();
-    // the next group's number (its atomic returned before the tile copy's wait)
-    const unsigned long long gnn = shfl0_u64(gnext);
+    // the next group's number (its atomic returned before the tile copy's wait; MULTI: taken at the group's end)
+    unsigned long long gnn = MULTI ? 0ull : shfl0_u64(gnext);
     const bool valid = lane < nvalid;
     const uint32_t* prow_mine = rows + (lane & (GROUP - 1)) * W;
     int nmsg = 0;
@@ -1199,6 +1174,10 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     // waits for them before.  (an asm-issued load's register was
     // invisible to the compiler.)
     uint32_t pfa = 0, pfb = 0;
+    if (MULTI) {
+      gnext = take_group();
+      gnn = shfl0_u64(gnext);
+    }
     while (KSPLIT && kpos - kdone + ccount > 0) {  // the group's last orbit keys (they key this group's rows)
       const int kc = min(kpos - kdone, 64 - ccount);
       key_chunk(kdone, kc, kc == 0 || kpos - kdone + ccount <= 64);  // (the last chunk: every image left)
@@ -1228,8 +1207,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       if (b != ~0ull) outbox_holes(box, o, b + used, b + OBOX_CHUNK, lane);
     }
   }
-  if (KSPLIT && (xflags & XF_SYM_QUEUE) && qb != ~0ull)
-    for (unsigned long long j = qb + qu + lane; j < min(qb + OBOX_CHUNK, box.cap); j += 64) box.send_ref[j] = ~0ull;
   for (int off = 32; off > 0; off >>= 1) {
     my_gen += __shfl_down(my_gen, off);
     my_probe += __shfl_down(my_probe, off);
@@ -1329,7 +1306,7 @@ static hipError_t launch_compact(const CompactArgs& a) {
   const uint64_t groups = (s_end - s_begin + GROUP - 1) / GROUP;
   uint64_t blocks = std::min<uint64_t>((groups + wpb - 1) / wpb, 1u << 20);
   const size_t lds = (size_t)wpb * compact_lds_words(L.W, L.all_words, GROUP, SYM, multi) * sizeof(uint32_t);
-  if (!(xflags & XF_NO_PERSIST)) {  // persistent waves: exactly the resident capacity, looping over groups
+  if (!(xflags & XF_NO_PERSIST) || a.query) {  // persistent waves: exactly the resident capacity, looping over groups
     static int per_cu[2][2];  // per instantiation: [multi][one-wave blocks]
     int& pc = per_cu[multi][wpb == 1];
     if (!pc) {
@@ -1339,6 +1316,11 @@ static hipError_t launch_compact(const CompactArgs& a) {
         if (atoi(e) > 0) pc = std::min(pc, atoi(e));
     }
     blocks = std::min<uint64_t>(blocks, (uint64_t)device_cus() * pc);
+    if (a.query) {  // level_kernel_shape: the waves resident at once (any launch mode) and the group size
+      a.query[0] = device_cus() * pc * wpb;
+      a.query[1] = GROUP;
+      return hipSuccess;
+    }
   }
   {
     hipError_t e = hipMemsetAsync(&ctr->group_next, 0, sizeof(ctr->group_next), st);

@@ -35,7 +35,7 @@ k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
   const unsigned long long p = blockIdx.y;  // owner shard
-  const unsigned long long n = counts[p];
+  const unsigned long long n = min(counts[p], cap);  // (reservations may run past the region: the overflow list)
   constexpr int SUB = 4;  // 64-record pieces per wave block: one next-level reservation for all their winners
   for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * (64ull * SUB); k0 < n;
        k0 += (unsigned long long)gridDim.x * wpb * 64ull * SUB) {

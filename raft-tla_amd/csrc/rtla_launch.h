@@ -33,7 +33,24 @@ struct CompactArgs {
   int xflags;
   uint64_t* sent;
   int wpb;
+  int* query = nullptr;  // non-null: store {waves launched at most, GROUP} of this launch, launch nothing
 };
+// The level kernel's shape for layout L (multi-shard or not): the most waves
+// one launch keeps resident and its frontier states per group.  false: the
+// layout runs the wave-per-state kernel (no group queue).
+bool level_kernel_shape(const Layout& L, bool multi, int xflags, int* waves, int* group);
+// Multi-shard exchange round: move the overflow list of the previous round
+// (in_fp / in_ref, *in_count records) into the outbox regions of `box` (slots
+// reserved on box.out_count); records whose region is full go to box's
+// overflow list.
+hipError_t launch_requeue(const uint64_t* in_fp, const uint64_t* in_ref, const uint64_t* in_count, uint64_t max_count,
+                          const ShardBox& box, DevCounters* ctr, hipStream_t st);
+// Multi-shard exchange round: out[G] = frontier states left for the next
+// round -- `rest` past the launch's range, plus those of its `span` states the
+// level kernel did not take (all taken unless `grouped`: then group_next *
+// group_size were) -- and out[G + 1] = records on the overflow list.
+hipError_t launch_round_tail(const DevCounters* ctr, uint64_t* out, int G, uint64_t span, uint64_t rest, bool grouped,
+                             const uint64_t* over_count, hipStream_t st);
 // The level kernel's instantiations, one translation unit each (compiled in
 // parallel): *done = false if the unit has no kernel for a.L.
 hipError_t launch_compact_spec_a(const CompactArgs& a, bool* done);     // configs[1], configs[0], exhaust
@@ -65,12 +82,6 @@ hipError_t launch_unpack_rows(int W, const uint32_t* rows, const uint64_t* count
                               uint64_t next_cap, DevCounters* ctr, uint64_t max_count, hipStream_t st);
 hipError_t launch_stage_rows(int W, const Ring& next, const uint64_t* parents, uint64_t next_base, uint64_t first,
                              uint64_t n, uint32_t* rows, hipStream_t st);
-// SYMMETRY, one shard: orbit keys + probes + new rows of the queued successors (rtla_ksymkeys.hip).
-bool launch_sym_keys_supported(const Layout& L);
-hipError_t launch_sym_keys(const Layout& L, const Ring& cur, uint64_t cur_base, const uint64_t* queue,
-                           const uint64_t* qcount, uint64_t qcap, const Ring& next, uint64_t* parents,
-                           uint64_t next_base, uint64_t next_cap, uint64_t* table, int tlog2, DevCounters* ctr,
-                           hipStream_t st);
 hipError_t launch_insert_rows(const Layout& L, const uint32_t* rows, uint64_t n, uint64_t* table,
                               int tlog2, int* new_flags, DevCounters* ctr, hipStream_t st);
 hipError_t launch_expand_batch(const Layout& L, const uint32_t* rows, uint64_t n, uint32_t* out,

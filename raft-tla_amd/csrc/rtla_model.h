@@ -329,10 +329,6 @@ RTLA_HD uint32_t m_f(uint64_t k, int lo, int bits) { return (uint32_t)(k >> lo) 
 struct FP {
   uint64_t a, b;
 };
-#ifdef RTLA_EXP_MIX1  // perf experiment only: one multiply per mix
-RTLA_HD uint64_t mix_a(uint64_t z) { z ^= z >> 32; z *= 0xbf58476d1ce4e5b9ull; return z ^ (z >> 29); }
-RTLA_HD uint64_t mix_b(uint64_t z) { z ^= z >> 31; z *= 0xff51afd7ed558ccdull; return z ^ (z >> 33); }
-#else
 RTLA_HD uint64_t mix_a(uint64_t z) {  // splitmix64 finalizer
   z ^= z >> 30; z *= 0xbf58476d1ce4e5b9ull;
   z ^= z >> 27; z *= 0x94d049bb133111ebull;
@@ -345,7 +341,6 @@ RTLA_HD uint64_t mix_b(uint64_t z) {  // murmur3 fmix64 (independent constants)
   z ^= z >> 33;
   return z;
 }
-#endif
 RTLA_HD FP fp_add(FP x, FP y) { return FP{x.a + y.a, x.b + y.b}; }
 RTLA_HD FP fp_sub(FP x, FP y) { return FP{x.a - y.a, x.b - y.b}; }
 RTLA_HD FP hash_u64(uint64_t tag, uint64_t x) {
@@ -1630,84 +1625,6 @@ RTLA_HD FP sym_image_fp(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, i
   }
   return f;
 }
-#ifndef RTLA_SYM_TWOPASS
-#define RTLA_SYM_TWOPASS 0
-#endif
-#if RTLA_SYM_TWOPASS
-// Experiment (round 4, measured slower inside the level kernel: its
-// register allocation at 3 waves/SIMD spilled the kernel into scratch,
-// 355 -> 987 ms per configs[3] step): the canonical image as the member
-// whose (server part, full fingerprint) pair is least -- the server parts of
-// all members first, the bag and elections hashed only for the members
-// tying on the least one.  Also an orbit invariant, with different key values.
-template <int NS, class RecF>
-RTLA_HD FP sym_image_srv_fp2(const Layout& L, RecF rec_of, const SymRank& r, int k, uint32_t* pim_o, uint32_t* inv_o) {
-  constexpr int SW = 3 + NS;
-  uint32_t pim = 0, invm = 0, used = 0;
-  int rem = k;
-#pragma unroll
-  for (int i = 0; i < NS; i++) {
-    const int rad = (int)pk_get<NS>(r.radm, i), cnt = (int)pk_get<NS>(r.cntm, i), lo = (int)pk_get<NS>(r.lom, i);
-    int dgt = 0;
-    if (rad > 1) {
-      dgt = rem % rad;
-      rem /= rad;
-    }
-    const uint32_t free = ((1u << cnt) - 1u) << lo & ~used;
-    int p = 0, c = dgt;
-#pragma unroll
-    for (int b = 0; b < NS; b++)
-      if (free >> b & 1u) {
-        if (c == 0) p = b;
-        c--;
-      }
-    pim |= (uint32_t)p << (3 * i);
-    invm |= (uint32_t)i << (3 * p);
-    used |= 1u << p;
-  }
-  FP f{0, 0};
-#pragma unroll 1
-  for (int i = 0; i < NS; i++) {
-    uint32_t rec[SW], out[SW];
-    rec_of(i, rec);
-    perm_srv_rec_p<NS>(rec, pim, invm, out);
-    f = fp_add(f, hash_words_from<SW>(srv_seed<NS>((int)pk_get<NS>(pim, i)), out));
-  }
-  *pim_o = pim;
-  *inv_o = invm;
-  return f;
-}
-template <int NS, class SlotF, class ElecF>
-RTLA_HD FP sym_image_rest_fp2(const Layout& L, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, uint32_t pim,
-                              uint32_t invm) {
-  constexpr int EW = 2 + NS;
-  FP f{0, 0};
-  for (int q = 0; q < nmsg; q++) f = fp_add(f, h_msg(perm_msg_slot_p<NS>(L, slot_of(q), pim)));
-  for (int e = 0; e < nelec; e++) {
-    uint32_t er[EW], out[EW];
-    elec_of(e, er);
-    perm_elec_p<NS>(er, pim, invm, out);
-    f = fp_add(f, h_elec(out, EW));
-  }
-  return f;
-}
-template <int NS, class RecF, class SlotF, class ElecF>
-RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
-                   int* perms = nullptr) {
-  const SymRank r = sym_rank<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of);
-  if (perms) *perms = r.ncomb;
-  FP bs{~0ull, ~0ull}, best{~0ull, ~0ull};
-  for (int k = 0; k < r.ncomb; k++) {
-    uint32_t pim, invm;
-    const FP sp = sym_image_srv_fp2<NS>(L, rec_of, r, k, &pim, &invm);
-    if (fp_less(bs, sp)) continue;
-    const FP f = fp_add(sp, sym_image_rest_fp2<NS>(L, nmsg, slot_of, nelec, elec_of, pim, invm));
-    if (fp_less(sp, bs) || fp_less(f, best)) best = f;
-    bs = sp;
-  }
-  return fp_add(orbit_key_finish(best), afp);
-}
-#else
 template <int NS, class RecF, class SlotF, class ElecF>
 RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of, FP afp,
                    int* perms = nullptr) {
@@ -1720,7 +1637,6 @@ RTLA_HD FP sym_key(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int ne
   }
   return fp_add(orbit_key_finish(best), afp);
 }
-#endif
 
 // allLogs part of a fingerprint: sum of h_all over the set bits of the words
 template <class Q>

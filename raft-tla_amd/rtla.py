@@ -23,6 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RTLA_LIB") or os.path.join(HERE, "librtla.so")  # RTLA_LIB: perf-experiment builds only
 
 OK, DONE, VIOLATION = 0, 1, 2
+E_CONFIG, E_HIP, E_OVERFLOW, E_SPEC, E_STATE, E_ARG, E_COMM = -1, -2, -3, -4, -5, -6, -7  # include/rtla.h
 INV_BITS = {"NoTwoLeaders": 1, "ElectionSafety": 2, "LogMatching": 4}
 COVER_NAMES = ["Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest",
                "AdvanceCommitIndex", "AppendEntries", "Receive", "DuplicateMessage",
@@ -328,7 +329,7 @@ def random_texts(cfg: Config, first: int, n: int, pool: int = 0, seed: int = SYN
     terminated by '\x1e' (rtla_random_texts; host)."""
     cc = cfg.c()
     need = C.c_size_t(0)
-    cap = n * 8192
+    cap = n * 2048  # a random state's text is ~1 KB; the rare larger batch is rendered again at its exact size
     buf = C.create_string_buffer(cap)
     if _lib.rtla_random_texts(C.byref(cc), seed, first, n, pool, buf, cap, C.byref(need)) != OK:
         buf = C.create_string_buffer(need.value + 1)
@@ -409,8 +410,8 @@ class Checker:
             pass
 
     def device_info(self) -> str:
-        buf = C.create_string_buffer(1024)
-        _check(_lib.rtla_device_info(self._h, buf, 1024), "rtla_device_info")
+        buf = C.create_string_buffer(4096)
+        _check(_lib.rtla_device_info(self._h, buf, 4096), "rtla_device_info")
         return buf.value.decode()
 
     def _rec(self, st: _Stats):

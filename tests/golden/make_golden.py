@@ -6,7 +6,7 @@ and the two must agree on every level's counts and state-text hash before the
 case is written.  The configs are the build's bounded models (specs/MC.tla);
 the reference ships no fixtures of its own.
 
-    python tests/golden/make_golden.py [--big] [--only=name,name]
+    python tests/golden/make_golden.py [--big] [--py-pins] [--only=name,name]
 """
 import json
 import os
@@ -67,6 +67,35 @@ SYM_PREFIXES = {
     "n4_v1_t2_l1_m1_sym_prefix": (4, 1, 2, 1, 1, 1, (NTL,), 3_000_000, 0),
     "n5_v1_t3_l2_c1_sym_prefix": (5, 1, 3, 2, 1, 0, (), 0, 15),
 }
+
+
+# The value oracle's own BFS over the first levels of the BASELINE prefixes
+# (the C oracle's fixtures above): per-level counts and content digests must
+# agree before "py_levels" is recorded -- the value semantics touch every
+# BASELINE shape (configs[0]-[3]; configs[3] through its orbit texts).
+# name: levels (as many as the pure-Python transcription finishes in minutes)
+PY_PINS = {
+    "n3_v1_t2_l1_c1_prefix": 11,      # configs[0]: 103,165 states
+    "n3_v2_t3_l2_c1_prefix": 9,       # configs[1]: 74,048 states
+    "n3_v2_t4_l3_c2_prefix": 8,       # configs[2]: 48,290 states
+    "n5_v1_t3_l2_c1_sym_prefix": 7,   # configs[3]: 1,501 orbits (all 120 images of every successor)
+}
+
+
+def pin_with_value_oracle(out, only):
+    for name, k in PY_PINS.items():
+        if (only and name not in only) or name not in out:
+            continue
+        g = out[name]
+        sym = bool(g.get("symmetry"))
+        pc = rv.Cfg(g["n_server"], g["n_value"], g["max_term"], g["max_log"], g["max_copies"],
+                    tuple(g["invariants"]), g["max_msgs"])
+        levels, hashes = rv.bfs_prefix(pc, k, symmetric=sym)
+        want = g["level_orbit_hash" if sym else "level_text_hash"]
+        assert [list(x) for x in levels] == g["levels"][:k], name
+        assert ["%016x" % h for h in hashes] == want[:k], name
+        g["py_levels"] = k
+        print(name, "value oracle agrees on the first %d levels" % k, flush=True)
 
 
 def main():
@@ -149,6 +178,8 @@ def main():
         print(name, r["distinct"], len(r["levels"]), "%.1fs" % r["seconds"], flush=True)
         with open(path, "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)
+    if "--py-pins" in sys.argv or big:
+        pin_with_value_oracle(out, only)
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

@@ -54,6 +54,35 @@ def main():
             out["seconds"] = time.time() - t0
         print(json.dumps(out), flush=True)
         return
+    mode = os.environ.get("RCCL_PAIR_MODE", "")
+    if mode.startswith("fault_"):
+        # RTLA_FAULT=<where>:<rank> makes that rank's local work at <where>
+        # fail: every rank must return an error from the same call, promptly
+        # (the failure travels in the call's reductions)
+        where = mode[len("fault_"):]
+        out = {"rank": rank}
+        with rtla.Checker(cfg, rank=rank, world=world, comm_id=cid) as ck:
+            st = ck.init()
+            t0 = time.time()
+            try:
+                while st == rtla.OK:
+                    st = ck.step()
+                out["step"] = st
+            except rtla.RtlaError as e:
+                out["step"] = e.status
+            if where != "exchange":
+                t0 = time.time()
+                try:
+                    if where == "coverage":
+                        ck.coverage()
+                    else:
+                        ck.trace()
+                    out[where] = 0
+                except rtla.RtlaError as e:
+                    out[where] = e.status
+            out["seconds"] = time.time() - t0
+        print(json.dumps(out), flush=True)
+        return
     with rtla.Checker(cfg, rank=rank, world=world, comm_id=cid) as ck:
         st = ck.init()
         while st == rtla.OK:

@@ -100,6 +100,41 @@ def test_lockstep_walk_successors_match_oracle(shape):
         assert rtla.invariants_violated(cfg, row) == walk.invariants()
 
 
+# BASELINE configs[0]-[3] shapes (N, V, T, L, C, in-flight bound) with the bag slots bench.py compiles for them
+BASELINE_WALKS = [((3, 1, 2, 1, 1, 0), 24), ((3, 2, 3, 2, 1, 0), 18), ((3, 2, 4, 3, 2, 0), 20), ((5, 1, 3, 2, 1, 0), 20)]
+
+
+@pytest.mark.parametrize("shape,bag", BASELINE_WALKS)
+def test_walk_successors_match_value_oracle(shape, bag):
+    """At every BASELINE shape, N = 5 (configs[3]) included: along a random
+    walk, the successor multiset the level kernel generates for a state
+    (rtla_expand_batch: k_expand_compact in its all-successors mode; texts and
+    in-model flags) equals the VALUE oracle's -- raft_values.next_states, the
+    literal transcription of raft.tla's Next -- on the state parsed from its
+    text; no C-oracle code in the loop."""
+    import tla_text
+    n, v, t, l, c, m = shape
+    cfg = rtla.Config(n, v, t, l, c, m, (), bag_cap=bag)
+    vc = rv.Cfg(n, v, t, l, c, (), m)
+    rnd = random.Random(sum(shape) * 17 + n)
+    row = rtla.init_row(cfg)
+    checked = 0
+    for step in range(60):
+        text = rtla.state_text(cfg, row)
+        ref = sorted((rv.in_model(vc, x), rv.state_text(vc, x))
+                     for _, x in rv.next_states(vc, tla_text.parse_state(vc, text)))
+        gpu = rtla.expand_batch(cfg, [row])
+        mine = sorted((bool(im), rtla.state_text(cfg, r)) for _, _, _, im, r in gpu)
+        assert mine == ref, "shape %s step %d" % (shape, step)
+        checked += len(mine)
+        # continue through an in-model successor whose bag leaves room for the next step
+        nxt = [x for x in gpu if x[3] and rtla.state_text(cfg, x[4]).split("\n", 1)[0].count(" :> ") < bag - 1]
+        if not nxt:
+            break
+        row = rnd.choice(nxt)[4]
+    assert checked > 300
+
+
 @pytest.mark.parametrize("shape", [(5, 1, 3, 2, 1, 0), (4, 1, 2, 1, 1, 2), (3, 2, 3, 2, 1, 3)])
 def test_symmetric_lockstep_walk_orbit_keys_match_oracle(shape):
     """SYMMETRY at the successor level, N = 5 (BASELINE configs[3]'s shape)
@@ -324,17 +359,58 @@ def test_many_shards_tiny_sent_cache_match_golden(name):
     slots, overwritten on a miss) are far smaller than the millions of
     fingerprints each ships: duplicates are re-sent and deduplicated by the
     owners -- the counts stay exact, and no capacity error is raised (the
-    overwrite-on-miss cache has no probe chain to run out of).  Also checks
-    that the level-end re-balancing kept the shards' levels within 2 % of an
-    even split."""
+    overwrite-on-miss cache has no probe chain to run out of).  After every
+    level the re-balancing leaves each shard within its threshold of an even
+    split (1 % of the level over the shards + 64 rows)."""
     g = GOLD[name]
     fpl = (g["distinct"] * 2).bit_length() - 3   # per shard: ~30-40 % load over the 8 shards
     cfg = cfg_of(g, shards=8, chunk=4096, fpset_log2=fpl, mem_budget=24 << 30)
     with rtla.Checker(cfg) as ck:
-        assert ck.run() == rtla.DONE
+        st = ck.init()
+        while st == rtla.OK:
+            st = ck.step()
+            shares = json.loads(ck.device_info())["shard_frontier"]
+            total = sum(shares)
+            if st == rtla.OK:
+                assert max(shares) <= total // 8 + 1 + 64 + total // 800, (len(ck.levels), shares)
+        assert st == rtla.DONE
         info = json.loads(ck.device_info())
         assert info["sent_cache_slots_log2"] == fpl - 2 and info["rebalanced_rows"] > 0
         assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
+
+
+@pytest.mark.parametrize("sent", [1, 0])
+@pytest.mark.parametrize("shards", [2, 8])
+@pytest.mark.parametrize("name", ["n3_v1_t2_l1_m1", "n3_v1_t2_l1_m1_sym", "n3_v1_t2_l1_m2"])
+def test_virtual_shards_tiny_outbox_match_golden(monkeypatch, name, shards, sent):
+    """Exchange rounds sized by the outbox (no chunk bound): with owner regions
+    of only 4096 records (RTLA_OUTBOX_CAP), every big level runs many rounds,
+    the level kernel's group guard stops it mid-level, and the records the
+    groups in flight still queue past a region's end take the overflow list
+    into the next round -- with and without the sent cache.  Golden counts
+    and level contents."""
+    monkeypatch.setenv("RTLA_OUTBOX_CAP", "4096")
+    monkeypatch.setenv("RTLA_SENT_CACHE", str(sent))
+    g = GOLD[name]
+    kw = dict(fpset_log2=max(16, (g["distinct"] * 2 // shards).bit_length()), mem_budget=24 << 30)
+    want, digest = level_digests(g) if g["distinct"] < 3_000_000 else ([], None)  # (the big model: counts)
+    with rtla.Checker(cfg_of(g, shards=shards, **kw)) as ck:
+        info = json.loads(ck.device_info())
+        assert info["outbox_records_per_owner"] == 4096 and (info["chunk"] == 0 or shards == 8)
+        assert info["sent_cache_slots_log2"] == (info["fpset_slots_log2"] - 2 if sent else 0)
+        st = ck.init()
+        got = []
+        while True:
+            if len(got) < len(want):
+                got.append("%016x" % digest(ck))
+            if st != rtla.OK:
+                break
+            st = ck.step()
+        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
+        assert got == want[:len(got)]
+        info = json.loads(ck.device_info())
+        assert info["exchange_rounds"] > len(g["levels"]) + 20, info  # (levels cut into several rounds)
+        assert info["overflowed_records"] > 0, info
 
 
 @pytest.mark.parametrize("shards", [2, 3, 8])
@@ -525,31 +601,6 @@ def test_symmetry_virtual_shards_match_golden(name, shards):
     res = rtla.check(cfg_of(g, shards=shards, chunk=700, **kw), trace=False)
     assert [[lv.new, lv.generated] for lv in res.levels] == g["levels"]
     assert (res.distinct, res.generated, res.depth) == (g["distinct"], g["generated"], g["depth"])
-
-
-@pytest.mark.parametrize("name", ["n3_v1_t2_l1_m1_sym", "n3_v1_t3_l1_m1_ntl_sym", "n4_v1_t2_l1_m1_sym_prefix"])
-def test_symmetry_key_kernel_matches_golden(monkeypatch, name):
-    """The separate SYMMETRY key kernel (RTLA_SYM_QUEUE=1: the level kernel
-    queues, k_sym_keys materialises, ranks, spreads the images over the
-    lanes, probes and builds): golden per-level orbit counts and orbit-text
-    digests, and the counterexample of the NoTwoLeaders model."""
-    monkeypatch.setenv("RTLA_SYM_QUEUE", "1")
-    g = GOLD[name]
-    kw = small_kw(g) if not g.get("prefix") else dict(fpset_log2=26)
-    want, digest = level_digests(g)
-    with rtla.Checker(cfg_of(g, **kw)) as ck:
-        assert json.loads(ck.device_info())["sym_key_queue"] > 0
-        st = ck.init()
-        got = []
-        while True:
-            got.append("%016x" % digest(ck))
-            if st != rtla.OK or len(ck.levels) >= len(g["levels"]):
-                break
-            st = ck.step()
-        assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
-        assert got == want[:len(got)] and len(got) >= len(want) - 1
-        if g.get("violated"):
-            assert st == rtla.VIOLATION and len(ck.trace()) == g["trace_len"]
 
 
 @pytest.mark.parametrize("shards", [1, 2])
@@ -829,6 +880,35 @@ def test_ranks_recover_fails_on_every_rank(tmp_path):
         assert p.returncode == 0, e[-2000:]
         outs.append(json.loads(o.strip().splitlines()[-1]))
     assert [o["recover"] for o in outs] == [-5, -6]  # the other rank's failure / the missing file
+    assert all(o["seconds"] < 30 for o in outs)
+
+
+@pytest.mark.parametrize("where,name", [("coverage", "n3_v1_t2_l1_m1"), ("trace", "n3_v1_t3_l1_m1_ntl"),
+                                        ("exchange", "n3_v1_t2_l1_m1")])
+def test_ranks_local_failure_fails_every_rank(tmp_path, where, name):
+    """One rank's local work fails (RTLA_FAULT=<where>:1) inside a collective
+    entry point -- the coverage read-back, a trace record, a level's exchange
+    rounds: every rank returns an error from that call, promptly, because the
+    failure travels in the call's reductions (no rank is left waiting in a
+    collective the failed rank never reaches)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, RTLA_TRANSPORT="shm", RTLA_SHM_SLOT_MB="32", RCCL_PAIR_MODE="fault_" + where,
+               RTLA_FAULT="%s:1" % where)
+    idfile = str(tmp_path / "comm_id")
+    helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_pair.py")
+    procs = [subprocess.Popen([sys.executable, helper, str(r), "2", idfile, name], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=120)
+        assert p.returncode == 0, e[-2000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    if where == "exchange":  # the level's reduction fails every rank: the local failure's status everywhere
+        assert [o["step"] for o in outs] == [rtla.E_HIP, rtla.E_HIP], outs
+    else:
+        assert outs[0]["step"] == outs[1]["step"] == (rtla.VIOLATION if where == "trace" else rtla.DONE)
+        assert [o[where] for o in outs] == [rtla.E_COMM, rtla.E_HIP], outs  # the peer's failure / its own
     assert all(o["seconds"] < 30 for o in outs)
 
 

@@ -177,3 +177,53 @@ def test_walk_orbit_texts_match_value_oracle(shape):
         if not inm:
             break
         w.goto(rnd.choice(inm))
+
+
+# The BASELINE configs' shapes (N, V, MaxTerm, MaxLogLen, MaxCopies, MaxInFlight):
+# configs[0] (raft.cfg bounds), configs[1], configs[2] (Duplicate/Drop live),
+# configs[3] (N = 5).
+BASELINE_SHAPES = [(3, 1, 2, 1, 1, 0), (3, 2, 3, 2, 1, 0), (3, 2, 4, 3, 2, 0), (5, 1, 3, 2, 1, 0)]
+
+
+@pytest.mark.parametrize("shape", BASELINE_SHAPES)
+def test_walk_successors_match_value_oracle(shape):
+    """Along a random walk at every BASELINE shape, N = 5 included: the C
+    oracle's successor multiset (state texts + in-model flags) of each state
+    equals the value oracle's (raft_values.next_states, the literal
+    transcription of raft.tla's Next) on the same state parsed from its text."""
+    import random
+    import tla_text
+    n, v, t, l, c, m = shape
+    vc = rv.Cfg(n, v, t, l, c, (), m)
+    w = raft_cpu.Walk(raft_cpu.cfg_of(n, v, t, l, c, m, ()))
+    rnd = random.Random(sum(shape) * 31 + n)
+    checked = 0
+    for step in range(60):
+        s = tla_text.parse_state(vc, w.text())
+        ref = sorted((rv.in_model(vc, x), rv.state_text(vc, x)) for _, x in rv.next_states(vc, s))
+        got = sorted(w.successors())
+        assert got == ref, "shape %s step %d" % (shape, step)
+        checked += len(got)
+        inm = [tx for im, tx in got if im]
+        if not inm:
+            break
+        w.goto(rnd.choice(inm))
+    assert checked > 300
+
+
+@pytest.mark.parametrize("name,levels", [("n3_v2_t3_l2_c1_prefix", 6), ("n5_v1_t3_l2_c1_sym_prefix", 5)])
+def test_value_oracle_pins_baseline_prefix(name, levels):
+    """The C oracle's BASELINE fixtures are pinned by the value oracle's own
+    BFS on their first levels (make_golden.py PY_PINS: every BASELINE prefix
+    carries py_levels >= 7); a short prefix is re-run here: per-level counts
+    and content digests (configs[3]: orbit counts and orbit-text digests)."""
+    for k in ("n3_v1_t2_l1_c1_prefix", "n3_v2_t3_l2_c1_prefix", "n3_v2_t4_l3_c2_prefix",
+              "n5_v1_t3_l2_c1_sym_prefix"):
+        assert GOLD[k].get("py_levels", 0) >= 7, k
+    g = GOLD[name]
+    sym = bool(g.get("symmetry"))
+    pc = rv.Cfg(g["n_server"], g["n_value"], g["max_term"], g["max_log"], g["max_copies"], tuple(g["invariants"]),
+                g["max_msgs"])
+    lv, hs = rv.bfs_prefix(pc, levels, symmetric=sym)
+    assert [list(x) for x in lv] == g["levels"][:levels]
+    assert ["%016x" % h for h in hs] == g["level_orbit_hash" if sym else "level_text_hash"][:levels]
