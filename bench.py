@@ -589,6 +589,12 @@ def main():
         "frontier_arena_rows": info.get("frontier_cap"), "row_bytes": levels[0].row_bytes,
         "rccl_ranks": info.get("world"),
     }
+    if world > 1 or args.shards > 1:  # the exchange over the whole run (warmup and timed steps, this rank)
+        fin = json.loads(run.ck.device_info())
+        config["exchange"] = {k: fin.get(k) for k in ("exchange_rounds", "records_sent", "overflowed_records",
+                                                      "outbox_records_per_owner", "sent_cache_slots_log2",
+                                                      "rebalanced_rows", "chunk")}
+        config["exchange"]["steps_counted"] = args.steps + args.warmup
     if run.capped:
         config["stopped_by"] = run.stop
         config["oracle_pinned"] = bool(run.pinned) and not args.cap_levels

@@ -148,6 +148,7 @@ struct rtla_ctx {
   uint64_t rebalanced = 0; // rows moved by level-end re-balancing (all levels, this process's shards)
   uint64_t rounds = 0;     // exchange rounds run (all levels)
   uint64_t overflowed = 0; // records that went through the overflow list (all levels, this process's shards)
+  uint64_t records = 0;    // fingerprint records this process's shards sent to other shards (all levels)
   uint64_t* red = nullptr;  // device scratch for all-reduces
   int level = 0;
   bool inited = false, finished = false;
@@ -1013,17 +1014,20 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   int tl = cfg->fpset_log2;
   if (!tl) {
     tl = 20;
-    // the fingerprint set (multi-shard: + the sent cache, a quarter of its size): ~40% of the budget
-    const uint64_t tshare = G > 1 ? per * 8 / 25 : per * 2 / 5;
+    // the fingerprint set (multi-shard: + the sent cache, half its size): ~40% of the budget
+    const uint64_t tshare = G > 1 ? per * 4 / 15 : per * 2 / 5;
     while (tl < 34 && (8ull << (tl + 1)) <= tshare) tl++;
   }
   if (tl < 10 || tl > 40) err = RTLA_E_CONFIG;
   x->tlog2 = tl;
   // the sent cache is a dedup hint (one slot per fingerprint, overwritten on
-  // a miss): a quarter of the set's slots; RTLA_SENT_CACHE=0 turns it off
-  // (every remote successor is queued for its owner)
+  // a miss): half the set's slots (configs[1], 8 shards: a quarter sends 8 %
+  // more records and takes 5 % longer, profiles/r05_v2); RTLA_SENT_CACHE=0
+  // turns it off (every remote successor is queued for its owner: 1.34x slower)
   const char* sc = getenv("RTLA_SENT_CACHE");
-  x->slog2 = sc && atoi(sc) == 0 ? 0 : std::max(12, tl - 2);
+  x->slog2 = sc && atoi(sc) == 0 ? 0 : std::max(12, tl - 1);
+  if (const char* sl = getenv("RTLA_SENT_LOG2"))  // experiments: the sent cache's size (log2 slots)
+    if (x->slog2 && atoi(sl) >= 12 && atoi(sl) <= 36) x->slog2 = atoi(sl);
   x->front_cap = cfg->frontier_cap;
   x->sh.resize(nlocal);
   for (int k = 0; k < nlocal && !err; k++) {
@@ -1062,12 +1066,13 @@ extern "C" int rtla_device_info(rtla_ctx* x, char* buf, size_t cap) {
            "\"fpset_slots_log2\": %d, \"frontier_cap\": %llu, \"row_words\": %d, \"grid\": %d, \"chunk\": %llu, "
            "\"transport\": \"%s\", \"sent_cache_slots_log2\": %d, \"rebalanced_rows\": %llu, "
            "\"outbox_records_per_owner\": %llu, \"overflow_records\": %llu, \"exchange_rounds\": %llu, "
-           "\"overflowed_records\": %llu, \"shard_frontier\": [%s]}",
+           "\"overflowed_records\": %llu, \"records_sent\": %llu, \"shard_frontier\": [%s]}",
            p.name, p.gcnArchName, p.multiProcessorCount, x->rank, x->world, x->nshard, x->tlog2,
            (unsigned long long)x->front_cap, x->L.W, x->grid, (unsigned long long)x->chunk,
            x->shm ? "shm" : x->comm ? (x->rccl_local ? "rccl-local" : "rccl") : "device", x->nshard > 1 ? x->slog2 : 0,
            (unsigned long long)x->rebalanced, (unsigned long long)x->box_cap, (unsigned long long)x->over_cap,
-           (unsigned long long)x->rounds, (unsigned long long)x->overflowed, fr.c_str());
+           (unsigned long long)x->rounds, (unsigned long long)x->overflowed, (unsigned long long)x->records,
+           fr.c_str());
   return RTLA_OK;
 }
 
@@ -1636,6 +1641,7 @@ extern "C" int rtla_step(rtla_ctx* x, rtla_level_stats* st) {
         s.pos = s.n_cur - x->h_rows[(size_t)s.id * RW + G];
         s.over_n = x->h_rows[(size_t)s.id * RW + G + 1];
         x->overflowed += s.over_n;
+        for (int p = 0; p < G; p++) x->records += s.h_out[p];
       }
       x->rounds++;
       if (left && !sent_recs && left >= last_left) {  // (cannot happen: a round with room takes a group)

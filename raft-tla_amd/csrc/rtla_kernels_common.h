@@ -492,6 +492,39 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
   return r;
 }
 
+// One build_all lane as a function of its own (SYMMETRY kernels): the new
+// state's full Delta, fingerprint and invariants, then the words in which its
+// row differs from the parent's copy (child_write; `wait`: the copies must
+// land first).  NOT inlined for the same reason as key_one: at the SYMMETRY
+// kernel's 128 VGPRs the inlined build pass is one of the two big spillers.
+#ifndef RTLA_SYM_BUILD_CALL
+#define RTLA_SYM_BUILD_CALL 1
+#endif
+struct BuildOut {
+  int bad, sub, in_model;
+};
+template <int NS, Layout LC, int GROUP>
+__device__ __noinline__ BuildOut build_one(const Layout& Lrt, const uint32_t* prow, int inst, FP qfp,
+                                           const uint32_t* pall_p, uint32_t* d1, uint32_t* base2, int n1, int off,
+                                           bool write, bool wait) {
+  const Layout& L = pick_layout<LC>(Lrt);
+  DeltaT<NS> d;
+  d.enabled = 0;
+  compute_delta<NS>(L, prow, inst, d);
+  const FP cfp = fp_add(qfp, delta_fp<NS>(L, prow, d));
+  BuildOut o{check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]), d.sub, d.in_model};
+  uint32_t spk[PACKW], epk[PACKW];
+  child_pack(L, d, spk, epk);
+  if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (write)
+    child_write(L, prow, d, spk, epk, StridedWords<GROUP>{const_cast<uint32_t*>(pall_p)}, cfp, [&](int w, uint32_t v) {
+      const int i = off + w;
+      if (i < n1) d1[i] = v;
+      else base2[i - n1] = v;
+    });
+  return o;
+}
+
 }  // namespace
 
 // RTLA_STAMPS (diagnostic builds only): per-wave cycle counts of the level
@@ -675,6 +708,38 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       const int e = act ? newl[(head + b + lane) & (NEWCAP - 1)] : 0;
       const int sl = e >> 8, inst = e & 255;
       const int child = b + lane;  // index in the run
+      if constexpr (SYM && RTLA_SYM_BUILD_CALL) {  // the lane's work as a call of its own (build_one)
+        BuildOut o{0, 0, 0};
+        if (act)
+          o = build_one<NS, LC, GROUP>(Lrt, rows + sl * W, inst, pfpl[sl], pall + sl, d1, next.base, n1, child * W,
+                                      rows_on && child < nrows, rows_on && b == 0);
+        else if (rows_on && b == 0)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!(xflags & XF_ALL_SUCCESSORS) && claim_violation(ctr, o.bad, lane)) {
+          ctr->viol_parent = cur_base + s0 + sl;
+          ctr->viol_inst = inst;
+          ctr->viol_in_model = 1;
+          ctr->viol_child = child < nrows ? next_base + obase + child : ~0ull;
+        }
+        if (!(xflags & XF_NO_COVER)) {
+          const int code = act ? cover_code(L, inst, o.sub) : -1;
+          const unsigned long long am = __ballot(act);
+          if (am) {
+            const int c0 = __shfl(code, __builtin_ctzll(am));
+            const bool same = act && code == c0;
+            const int n0 = __popcll(__ballot(same));
+            if (lane == 0) atomicAdd(&cov[COVER_CODES + c0], (unsigned)n0);
+            if (act && !same) atomicAdd(&cov[COVER_CODES + code], 1u);
+          }
+        }
+        if (child < nrows && RTLA_IDX_OK(ctr, next_base + obase + child, ctr->cap_parents))
+          parents[next_base + obase + child] =
+              (xflags & XF_ALL_SUCCESSORS)
+                  ? (cur_base + s0 + sl) << 32 | (unsigned long long)(o.in_model ? 1u : 0u) << 31 |
+                        (unsigned long long)o.sub << 16 | (unsigned long long)inst
+                  : (unsigned long long)me << 56 | (cur_base + s0 + sl) << 16 | (unsigned long long)inst;
+        continue;
+      }
       DeltaT<NS> d;
       d.enabled = 0;
       if (act) compute_delta<NS>(L, rows + sl * W, inst, d);
@@ -763,7 +828,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       if (pend) {  // this chunk's load -> seen, or a CAS (sent cache: a store) for the next issue
         const bool to_sent = MULTI && powner != me;
         const int lg = to_sent ? box.slog2 : tlog2;
-        const unsigned long long key = pf.b | 1ull, idx = home_slot(pf, lg);
+        const unsigned long long key = pf.b | 1ull, idx = to_sent ? home_slot(pf, lg) : pf.a >> (64 - lg);
         if (pold != key) {
           cidx = (to_sent || pold == 0ull) ? idx : ((idx + 1ull) & ((1ull << lg) - 1ull));
           ckey = key;
@@ -932,7 +997,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
           nprobe = !(xflags & XF_NO_PROBE);
           ncf = key;
           nowner = MULTI ? fp_owner(key, box.nshard) : me;
-          nidx = home_slot(key, (MULTI && nowner != me) ? box.slog2 : tlog2);
+          nidx = (MULTI && nowner != me) ? home_slot(key, box.slog2) : key.a >> (64 - tlog2);
         }
       }
     }
@@ -1004,7 +1069,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
         nprobe = !(xflags & XF_NO_PROBE);
         ncf = key;
         nowner = MULTI ? fp_owner(key, box.nshard) : me;
-        nidx = home_slot(key, (MULTI && nowner != me) ? box.slog2 : tlog2);
+        nidx = (MULTI && nowner != me) ? home_slot(key, box.slog2) : key.a >> (64 - tlog2);
       }
     }
     const unsigned long long cm = __ballot(next >= 0);
@@ -1086,7 +1151,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     if (!__ballot(full) && lane == 0) g = atomicAdd(&ctr->group_next, 1ull);
     return g;
   };
-  if (blockIdx.x == 0 && lane == 0 && wave == 0) ctr->group_size = GROUP;
+  if (MULTI && blockIdx.x == 0 && lane == 0 && wave == 0) ctr->group_size = GROUP;
   unsigned long long gnext = 0;
   if (MULTI) gnext = take_group();
   else if (lane == 0) gnext = atomicAdd(&ctr->group_next, 1ull);

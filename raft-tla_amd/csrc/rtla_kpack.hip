@@ -13,6 +13,10 @@
 // frontiers are (rtla_step re-balances what drifts).  Invariants and
 // distinct coverage are evaluated here, where parent and action are known.
 // LC: compiled-in layout (Layout{} = run-time Lrt), as for the level kernel.
+constexpr int BW_QUEUE = 128;  // per-wave LDS queue of winner refs (u64): batches of 64 winners
+__host__ __device__ constexpr int build_winners_lds_words(int W, int AW) {
+  return lane_lds_words(W, AW) + 2 * BW_QUEUE;
+}
 template <int NS, Layout LC>
 __global__ void __launch_bounds__(256)
 k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
@@ -20,86 +24,80 @@ k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
                 const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap, Ring next,
                 unsigned long long* __restrict__ parents, unsigned long long next_base, unsigned long long next_cap,
                 DevCounters* ctr) {
-  // A wave scans 64 records of owner p (grid.y), compacts the winners,
+  // A wave scans 64 records of owner p (grid.y) at a time and queues the
+  // winners' refs in LDS; every 64 queued winners -- one full wave -- it
   // gathers their parent rows into LDS (one coalesced read per row), builds
   // each successor in place, reserves next-level slots with one atomic and
-  // stores the rows (one coalesced write per row) and parent records.
+  // stores the rows (one coalesced write per row) and parent records.  (A
+  // batch per 64 records instead would run compute_delta on the ~quarter of
+  // the lanes whose record won.)
   const Layout& L = pick_layout<LC>(Lrt);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[COVER_CODES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
   const int W = L.W, AW = L.all_words;
-  uint32_t* lrows = lds + wave * lane_lds_words(W, AW);
+  uint32_t* lrows = lds + wave * build_winners_lds_words(W, AW);
   const LaneWords pall{lrows + 64 * W + lane};
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(lrows + lane_lds_words(W, AW));
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x) cov[k] = 0;
   __syncthreads();
   const unsigned long long p = blockIdx.y;  // owner shard
   const unsigned long long n = min(counts[p], cap);  // (reservations may run past the region: the overflow list)
-  constexpr int SUB = 4;  // 64-record pieces per wave block: one next-level reservation for all their winners
-  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * (64ull * SUB); k0 < n;
-       k0 += (unsigned long long)gridDim.x * wpb * 64ull * SUB) {
-    unsigned long long mk[SUB];
-    int tot = 0;
-#pragma unroll
-    for (int u = 0; u < SUB; u++) {
-      const unsigned long long k = k0 + u * 64ull + lane;
-      mk[u] = __ballot(k < n && ans[p * cap + k] != 0u);
-      tot += __popcll(mk[u]);
-    }
-    if (!tot) continue;
+  // build the first nw queued winners (q[0, nw): parent index << 16 | instance)
+  auto build = [&](int nw) {
     unsigned long long obase = 0;
-    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)tot);
+    if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)nw);
     obase = shfl0_u64(obase);
-    if (obase + tot > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
-    for (int u = 0; u < SUB; u++) {
-      const unsigned long long m = mk[u];
-      if (!m) continue;
-      const int nw = __popcll(m);
-      // lane r takes the r-th winner's record
-      int src_lane = 0;
-      {
-        unsigned long long mm = m;
-        for (int r = 0; r < nw; r++) {
-          const int l = __builtin_ctzll(mm);
-          mm &= mm - 1;
-          if (lane == r) src_lane = l;
-        }
+    if (obase + nw > next_cap && lane == 0) set_flag(ctr, FLAG_FRONTIER_FULL);
+    const bool act = lane < nw;
+    const unsigned long long ref = act ? q[lane] : 0ull;
+    const unsigned long long s = ref >> 16;  // parent: state s of the current level
+    const int inst = (int)(ref & 0xffffull);
+    gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
+    wave_sync();
+    uint32_t* prow = lrows + lane * W;
+    if (act) {
+      const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
+      DeltaT<NS> d;
+      compute_delta<NS>(L, prow, inst, d);
+      const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
+      const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
+      if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+          atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
+        ctr->viol_parent = cur_base + s;
+        ctr->viol_inst = inst;
+        ctr->viol_in_model = 1;
+        ctr->viol_child = obase + lane < next_cap ? next_base + obase + lane : ~0ull;
       }
-      const unsigned long long i = p * cap + k0 + u * 64ull + lane;
-      const unsigned long long ref = shfl_u64((m >> lane & 1ull) ? send_ref[i] : 0ull, src_lane);
-      const bool act = lane < nw;
-      const unsigned long long s = ref >> 16;  // parent: state s of the current level
-      const int inst = (int)(ref & 0xffffull);
-      gather_rows_lds(lrows, W, nw, [&](int r) { return ring_row(cur, readlane_u64(s, r), W); }, lane);
-      wave_sync();
-      uint32_t* prow = lrows + lane * W;
-      if (act) {
-        const FP pfp = fp_add(row_fp(prow), alllogs_delta<NS>(L, prow, pall));
-        DeltaT<NS> d;
-        compute_delta<NS>(L, prow, inst, d);
-        const FP cfp = fp_add(pfp, delta_fp<NS>(L, prow, d));
-        const int bad = check_invariants_v<NS>(L, prow, d.srv, d.rec[0], d.rec[1], d.elec, d.erec[0]);
-        if (bad && __hip_atomic_load(&ctr->viol_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-            atomicCAS(&ctr->viol_mask, 0, bad) == 0) {
-          ctr->viol_parent = cur_base + s;
-          ctr->viol_inst = inst;
-          ctr->viol_in_model = 1;
-          ctr->viol_child = obase + lane < next_cap ? next_base + obase + lane : ~0ull;
-        }
-        atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
-        materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
-      }
-      wave_sync();
-      const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nw, next_cap - obase);
-      store_rows_ring(next, obase, nrows, W, lrows, lane);
-      if (lane < nrows)
-        parents[next_base + obase + lane] =
-            (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
-      obase += nw;
+      atomicAdd(&cov[cover_code(L, inst, d.sub)], 1u);
+      materialize<NS>(L, prow, d, pall, cfp, prow);  // in place
+    }
+    wave_sync();
+    const int nrows = obase >= next_cap ? 0 : (int)min<unsigned long long>((unsigned long long)nw, next_cap - obase);
+    store_rows_ring(next, obase, nrows, W, lrows, lane);
+    if (lane < nrows)
+      parents[next_base + obase + lane] = (unsigned long long)me << 56 | (cur_base + s) << 16 | (unsigned long long)inst;
+    wave_sync();
+  };
+  int qn = 0;  // winners queued (wave-uniform)
+  const unsigned long long lanes_below = (1ull << lane) - 1ull;
+  for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; k0 < n;
+       k0 += (unsigned long long)gridDim.x * wpb * 64ull) {
+    const unsigned long long k = k0 + lane;
+    const bool win = k < n && ans[p * cap + k] != 0u;
+    const unsigned long long m = __ballot(win);
+    if (win) q[qn + __popcll(m & lanes_below)] = send_ref[p * cap + k];
+    qn += __popcll(m);
+    wave_sync();
+    if (qn >= 64) {
+      build(64);
+      qn -= 64;
+      if (lane < qn) q[lane] = q[64 + lane];  // (the rest moves to the front: fewer than 64)
       wave_sync();
     }
   }
+  if (qn) build(qn);
   __syncthreads();
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
     if (cov[k]) atomicAdd(&ctr->cover[COVER_CODES + k], (unsigned long long)cov[k]);
@@ -173,9 +171,10 @@ static hipError_t build_winners(const Layout& L, const Ring& cur, uint64_t cur_b
                                 const uint32_t* ans, const uint64_t* counts, int nshard, uint64_t cap, const Ring& next,
                                 uint64_t* parents, uint64_t next_base, uint64_t next_cap, DevCounters* ctr,
                                 uint64_t max_count, hipStream_t st) {
-  const int wpb = std::max(1, expand_lane_wpb(L));
-  const size_t lds = (size_t)wpb * lane_lds_words(L.W, L.all_words) * sizeof(uint32_t);
-  hipLaunchKernelGGL((k_build_winners<NS, LC>), dim3(grid_x(max_count, 256 * wpb), nshard), dim3(64 * wpb), lds, st,
+  const size_t per = (size_t)build_winners_lds_words(L.W, L.all_words) * sizeof(uint32_t);
+  const int wpb = per * 4 <= 64 * 1024 ? 4 : (per * 2 <= 64 * 1024 ? 2 : 1);
+  const size_t lds = (size_t)wpb * per;
+  hipLaunchKernelGGL((k_build_winners<NS, LC>), dim3(grid_x(max_count, 1024 * wpb), nshard), dim3(64 * wpb), lds, st,
                      L, cur, (unsigned long long)cur_base, me, (const unsigned long long*)send_ref, ans,
                      (const unsigned long long*)counts, nshard, (unsigned long long)cap, next,
                      (unsigned long long*)parents, (unsigned long long)next_base, (unsigned long long)next_cap, ctr);

@@ -355,7 +355,7 @@ def test_virtual_shards_match_golden(name, shards):
 
 @pytest.mark.parametrize("name", ["n3_v1_t2_l1_m2", "n3_v1_t2_l1_m2_sym"])
 def test_many_shards_tiny_sent_cache_match_golden(name):
-    """8 fingerprint-owned shards whose sent caches (2^(fpset_log2 - 2)
+    """8 fingerprint-owned shards whose sent caches (2^(fpset_log2 - 1)
     slots, overwritten on a miss) are far smaller than the millions of
     fingerprints each ships: duplicates are re-sent and deduplicated by the
     owners -- the counts stay exact, and no capacity error is raised (the
@@ -375,7 +375,7 @@ def test_many_shards_tiny_sent_cache_match_golden(name):
                 assert max(shares) <= total // 8 + 1 + 64 + total // 800, (len(ck.levels), shares)
         assert st == rtla.DONE
         info = json.loads(ck.device_info())
-        assert info["sent_cache_slots_log2"] == fpl - 2 and info["rebalanced_rows"] > 0
+        assert info["sent_cache_slots_log2"] == fpl - 1 and info["rebalanced_rows"] > 0
         assert [[lv.new, lv.generated] for lv in ck.levels] == g["levels"]
 
 
@@ -397,7 +397,7 @@ def test_virtual_shards_tiny_outbox_match_golden(monkeypatch, name, shards, sent
     with rtla.Checker(cfg_of(g, shards=shards, **kw)) as ck:
         info = json.loads(ck.device_info())
         assert info["outbox_records_per_owner"] == 4096 and (info["chunk"] == 0 or shards == 8)
-        assert info["sent_cache_slots_log2"] == (info["fpset_slots_log2"] - 2 if sent else 0)
+        assert info["sent_cache_slots_log2"] == (info["fpset_slots_log2"] - 1 if sent else 0)
         st = ck.init()
         got = []
         while True:

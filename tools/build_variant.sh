@@ -10,7 +10,7 @@ D=$ROOT/exp/$name; rm -rf $D; mkdir -p $D
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wno-unused-result $*"
 S=${SRC:-$ROOT/raft-tla_amd/csrc}  # SRC: a modified copy of csrc/ (its ../../include must hold rtla.h)
-ALL="rtla_kernels rtla_kwave rtla_kpack rtla_kspec_a rtla_kspec_b rtla_ksym_a rtla_ksym_b rtla_kgeneric_a rtla_kgeneric_b"
+ALL=${ALL_UNITS:-"rtla_kernels rtla_kwave rtla_kpack rtla_kspec_a rtla_kspec_b rtla_ksym_a rtla_ksym_b rtla_kgeneric_a rtla_kgeneric_b"}
 pids=""
 if [ -n "$UNITS" ]; then
   for u in $ALL rtla_host rtla_text; do cp $ROOT/raft-tla_amd/build/$u.o $D/$u.o; done
