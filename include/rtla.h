@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTLA_ABI_VERSION 8
+#define RTLA_ABI_VERSION 9
 
 /* status codes */
 #define RTLA_OK 0
@@ -85,8 +85,16 @@ typedef struct {
                               rounded down to a multiple of 64); 0 = all HBM left after the other
                               structures */
     uint64_t mem_budget;   /* bytes of HBM this context may use; 0 = 85% of free */
-    uint64_t chunk;        /* multi-shard: frontier states expanded per exchange round; 0 = auto */
+    uint64_t chunk;        /* multi-shard: at most this many frontier states expanded per exchange
+                              round; 0 = as many as the outbox allows */
+    int32_t mode;          /* RTLA_MODE_BFS (0), or RTLA_MODE_DEDUP: a context for the synthetic
+                              microbench only (rtla_synthetic_*; no parent records, so no BFS:
+                              rtla_init / rtla_step return RTLA_E_STATE) */
+    int32_t reserved;      /* 0 */
 } rtla_cfg;
+
+#define RTLA_MODE_BFS 0
+#define RTLA_MODE_DEDUP 1
 
 typedef struct {
     int32_t level;            /* BFS level whose states were just produced (Init = 1) */

@@ -1720,6 +1720,8 @@ typedef struct {
     uint64_t *cnt;   /* per thread: gen, probes, new */
     int tid_next;
     pthread_mutex_t mu;
+    State *states;   /* the inputs, parsed before the timed phase */
+    int parse;       /* 1: the workers parse texts -> states; 0: they expand + deduplicate states */
 } DedupJob;
 typedef struct { DedupJob *j; int tid; uint8_t *pser; size_t plen; uint8_t *ser; } DedupEmit;
 static void dedup_emit(void *ud, const State *t, int action, int arg) {
@@ -1740,17 +1742,21 @@ static void *dedup_worker(void *arg) {
     pthread_mutex_lock(&j->mu);
     DedupEmit e = {j, j->tid_next++, NULL, 0, NULL};
     pthread_mutex_unlock(&j->mu);
-    State *s = (State *)malloc(sizeof(State)), *t = (State *)malloc(sizeof(State)), *base = (State *)malloc(sizeof(State));
+    State *t = (State *)malloc(sizeof(State)), *base = (State *)malloc(sizeof(State));
     e.pser = (uint8_t *)malloc(1 << 17);
     e.ser = (uint8_t *)malloc(1 << 17);
     for (;;) {
         const size_t i = atomic_fetch_add(&j->next, 1);
         if (i >= j->n) break;
-        if (parse_state(&j->d->c, j->texts[i], s)) { atomic_store(&j->err, 1); break; }
+        State *s = &j->states[i];
+        if (j->parse) {
+            if (parse_state(&j->d->c, j->texts[i], s)) { atomic_store(&j->err, 1); break; }
+            continue;
+        }
         e.plen = serialize(&j->d->c, s, e.pser);
         expand(&j->d->c, s, base, t, dedup_emit, &e);
     }
-    free(s); free(t); free(base); free(e.pser); free(e.ser);
+    free(t); free(base); free(e.pser); free(e.ser);
     return NULL;
 }
 void *orc_dedup_new(const orc_cfg *c) {
@@ -1766,8 +1772,9 @@ void orc_dedup_free(void *h) {
     free(d);
 }
 /* Expand + dedup the states of `texts` ('\x1e'-terminated state texts, n of
- * them), threads workers; out[0..2] += generated, probes, new; out[3] =
- * seconds of this call.  Returns 0, or -1 on a text it cannot parse. */
+ * them), threads workers; out[0..2] += generated, probes, new; *seconds =
+ * the expand + dedup phase (the texts are parsed before it, untimed).
+ * Returns 0, or -1 on a text it cannot parse. */
 int orc_dedup_texts(void *h, const char *texts, size_t n, int threads, uint64_t *out, double *seconds) {
     Dedup *d = (Dedup *)h;
     g_overflow = 0; g_spec_error = 0;
@@ -1787,15 +1794,26 @@ int orc_dedup_texts(void *h, const char *texts, size_t n, int threads, uint64_t 
     j.d = d; j.texts = v; j.n = n;
     atomic_store(&j.next, 0); atomic_store(&j.err, 0);
     j.cnt = (uint64_t *)calloc((size_t)threads * 3, 8);
+    j.states = (State *)malloc(sizeof(State) * (n ? n : 1));
     pthread_mutex_init(&j.mu, NULL);
-    const double t0 = now_s();
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    /* the texts are parsed first, outside the timed phase (the GPU leg is
+       handed packed rows: it parses nothing) */
+    j.parse = 1;
     for (int k = 0; k < threads; k++) pthread_create(&th[k], NULL, dedup_worker, &j);
     for (int k = 0; k < threads; k++) pthread_join(th[k], NULL);
+    j.parse = 0;
+    j.tid_next = 0;
+    atomic_store(&j.next, 0);
+    const double t0 = now_s();
+    if (!atomic_load(&j.err)) {
+        for (int k = 0; k < threads; k++) pthread_create(&th[k], NULL, dedup_worker, &j);
+        for (int k = 0; k < threads; k++) pthread_join(th[k], NULL);
+    }
     if (seconds) *seconds = now_s() - t0;
     for (int k = 0; k < threads; k++)
         for (int x = 0; x < 3; x++) out[x] += j.cnt[3 * k + x];
-    free(th); free(j.cnt); free(v); free(buf);
+    free(th); free(j.cnt); free(j.states); free(v); free(buf);
     pthread_mutex_destroy(&j.mu);
     return atomic_load(&j.err) || g_overflow || g_spec_error ? -1 : 0;
 }

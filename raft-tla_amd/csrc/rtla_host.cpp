@@ -832,7 +832,8 @@ static int alloc_shard(rtla_ctx* x, Shard& s, uint64_t budget) {
   const Layout& L = x->L;
   const int G = x->nshard;
   uint64_t tbytes = 8ull << x->tlog2;
-  s.parents_cap = (1ull << x->tlog2) - (1ull << x->tlog2) / 4;  // load factor <= 0.75
+  // load factor <= 0.75 (RTLA_MODE_DEDUP: no BFS, no parent records)
+  s.parents_cap = x->cfg.mode == RTLA_MODE_DEDUP ? 64 : (1ull << x->tlog2) - (1ull << x->tlog2) / 4;
   uint64_t pbytes = s.parents_cap * 8;
   uint64_t rowb = (uint64_t)L.W * 4;
   uint64_t boxb = G > 1 ? (uint64_t)G * x->box_cap * (16 + 8 + 4 + 16 + 4) +
@@ -954,6 +955,8 @@ extern "C" int rtla_open(const rtla_cfg* cfg, int rank, int world, const void* c
   if (world > 1 && !comm_id) return RTLA_E_ARG;
   if (world > 1 && cfg->shards > 1) return RTLA_E_CONFIG;
   if (world > SHARD_MAX || cfg->shards > SHARD_MAX) return RTLA_E_CONFIG;  // per-owner outbox state is sized by it
+  if (cfg->mode != RTLA_MODE_BFS && (cfg->mode != RTLA_MODE_DEDUP || world > 1 || cfg->shards > 1))
+    return RTLA_E_CONFIG;
   rtla_ctx* x = new rtla_ctx();
   x->cfg = *cfg;
   int r = layout_from_cfg(cfg, &x->L);
@@ -1220,6 +1223,7 @@ extern "C" int rtla_checkpoint(rtla_ctx* x, const char* prefix) {
 
 extern "C" int rtla_recover(rtla_ctx* x, const char* prefix) {
   if (!x || !prefix) return RTLA_E_ARG;
+  if (x->cfg.mode == RTLA_MODE_DEDUP) return RTLA_E_STATE;
   std::vector<char> buf(64 << 20);
   int level = -1;
   int err = hipSetDevice(x->device) != hipSuccess ? RTLA_E_HIP : RTLA_OK;  // the first local failure
@@ -1287,7 +1291,7 @@ extern "C" int rtla_reset(rtla_ctx* x) {
 
 extern "C" int rtla_init(rtla_ctx* x, rtla_level_stats* st) {
   if (!x) return RTLA_E_ARG;
-  if (x->inited) return RTLA_E_STATE;
+  if (x->inited || x->cfg.mode == RTLA_MODE_DEDUP) return RTLA_E_STATE;
   double t0 = now_s();
   HIPCHK(hipSetDevice(x->device));
   const Layout& L = x->L;

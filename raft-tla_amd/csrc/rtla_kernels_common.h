@@ -283,6 +283,58 @@ __device__ __forceinline__ int successor_orbit_step(const Layout& L, P prow, con
   });
 }
 
+// a[j] += v for a run-time j (selects)
+template <int NS>
+__device__ __forceinline__ void add_at(uint32_t* a, uint32_t j, uint32_t v) {
+#pragma unroll
+  for (int k = 0; k < NS; k++)
+    if ((uint32_t)k == j) a[k] += v;
+}
+// successor_orbit_step with the successor's signatures PATCHED from the
+// parent's parts (psg[w * S], w < 3 * NS: srv_sig, sent and received message
+// sums per server, computed once per parent row): the changed server's local
+// part is recomputed, each bag write moves its old slot's share out of and
+// its new slot's share into the sums -- no pass over the successor's bag and
+// records.  The same signatures, hence the same key, as sym_rank's.
+template <int NS, int S, class P>
+__device__ __forceinline__ int successor_orbit_step_sig(const Layout& L, P prow, const DeltaT<NS>& d,
+                                                        const uint32_t* psg, int k, bool all, FP& best) {
+  return with_successor<NS>(L, prow, d, [&](auto rec_of, int nmsg, auto slot_of, int nelec, auto elec_of) {
+    uint32_t ms[NS], mr[NS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+      ms[j] = psg[(NS + j) * S];
+      mr[j] = psg[(2 * NS + j) * S];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      if (q >= d.nops) continue;
+      const uint64_t o = d.op_old[q], v = d.op_new[q];
+      if (o) {
+        const uint32_t c = slot_sig_sent(L, o);
+        add_at<NS>(ms, slot_src(L, o), 0u - c);
+        add_at<NS>(mr, slot_dst(L, o), 0u - slot_sig_recv(c));
+      }
+      if (v) {
+        const uint32_t c = slot_sig_sent(L, v);
+        add_at<NS>(ms, slot_src(L, v), c);
+        add_at<NS>(mr, slot_dst(L, v), slot_sig_recv(c));
+      }
+    }
+    const uint32_t lsrv = d.srv >= 0 ? srv_sig<NS>(d.srv, d.rec) : 0u;
+    uint64_t sig[NS];
+#pragma unroll
+    for (int i = 0; i < NS; i++) sig[i] = sig_of(i == d.srv ? lsrv : psg[i * S], ms[i], mr[i]);
+    const SymRank r = sym_rank_from<NS>(L, sig, rec_of, nmsg, slot_of, nelec, elec_of);
+    const int k1 = all ? r.ncomb : min(k + 1, r.ncomb);
+    for (int j = k; j < k1; j++) {
+      const FP f = sym_image_fp<NS>(L, rec_of, nmsg, slot_of, nelec, elec_of, r, j);
+      if (fp_less(f, best)) best = f;
+    }
+    return k1 < r.ncomb ? k1 : -1;
+  });
+}
+
 // Load the parent row into LDS and derive the per-parent data every lane
 // needs.  Returns the parent fingerprint with allLogs' already applied.
 template <int NS>
@@ -367,7 +419,7 @@ constexpr int NEWFLUSH = NEWCAP - 3 * 64;
 // stays small enough for 12 one-wave blocks per CU on configs[1]'s 372-byte rows.)
 __host__ __device__ constexpr int compact_lds_words(int W, int AW, int GROUP, bool sym, bool multi) {
   return (4 * GROUP * (sym ? 2 : 1) + (multi ? 4 * SHARD_MAX : 0) + NEWCAP / 2 + GROUP * W + GROUP * AW +
-          RING / 2 * (sym ? 2 : 1) + (sym ? 5 * 64 : 0) + 3) & ~3;
+          RING / 2 * (sym ? 2 : 1) + (sym ? 5 * 64 + 3 * NMAX * GROUP : 0) + 3) & ~3;
 }
 
 // bits << off into a 64-bit window mask (off may be negative or >= 64)
@@ -474,9 +526,9 @@ struct KeyStep {
   FP f;
   int next;
 };
-template <int NS, Layout LC>
-__device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow, int inst, int k, bool all, FP best0,
-                                        FP afp) {
+template <int NS, Layout LC, int S>
+__device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow, const uint32_t* psg, int inst, int k,
+                                        bool all, FP best0, FP afp) {
   const Layout& L = pick_layout<LC>(Lrt);
   DeltaT<NS> d;
   d.enabled = 0;
@@ -487,7 +539,7 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
     return r;
   }
   FP best = best0;
-  r.next = successor_orbit_step<NS>(L, prow, d, k, all, best);
+  r.next = successor_orbit_step_sig<NS, S>(L, prow, d, psg, k, all, best);
   r.f = r.next < 0 ? fp_add(orbit_key_finish(best), afp) : best;
   return r;
 }
@@ -606,6 +658,9 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   FP* cbest = reinterpret_cast<FP*>(kring + (SYM ? RING : 0));
   uint32_t* cent = reinterpret_cast<uint32_t*>(cbest + (SYM ? 64 : 0));
   int ccount = 0;
+  // SYMMETRY: each tile row's signature parts (sym_sig_parts: srv_sig, sent
+  // and received message sums per server), word w of row r at sigl[w * GROUP + r]
+  uint32_t* sigl = cent + (SYM ? 64 : 0);
   if (MULTI) {
     if (lane < SHARD_MAX) {
       obox[lane] = ~0ull;
@@ -1061,7 +1116,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     int next = -1;
     FP best{~0ull, ~0ull};
     if (active) {
-      const KeyStep ks = key_one<NS, LC>(Lrt, prow, inst, k, last, cont ? cbest[lane] : FP{~0ull, ~0ull}, afpl[sl]);
+      const KeyStep ks = key_one<NS, LC, GROUP>(Lrt, prow, sigl + sl, inst, k, last,
+                                                cont ? cbest[lane] : FP{~0ull, ~0ull}, afpl[sl]);
       next = ks.next < 0 ? -1 : ks.next;
       best = ks.f;
       if (ks.next == -1) {
@@ -1176,6 +1232,17 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       pfpl[lane] = fp_add(row_fp(prow_mine), alllogs_delta<NS>(L, prow_mine, pall_mine));
       if (SYM) afpl[lane] = alllogs_fp(L, pall_mine);
       nmsg = row_nmsg(L, prow_mine);
+      if constexpr (KSPLIT) {
+        uint32_t loc[NS], ms[NS], mr[NS];
+        sym_sig_parts<NS>(L, [&](int i, uint32_t* out) { load_rec<NS>(L, prow_mine, i, out); }, nmsg,
+                          [&](int q) { return slot_raw(L, prow_mine, q); }, loc, ms, mr);
+#pragma unroll
+        for (int j = 0; j < NS; j++) {
+          sigl[j * GROUP + lane] = loc[j];
+          sigl[(NS + j) * GROUP + lane] = ms[j];
+          sigl[(2 * NS + j) * GROUP + lane] = mr[j];
+        }
+      }
     }
     wave_sync();
     STAMP(0);  // group start: work-queue atomic, row tile load, per-state setup

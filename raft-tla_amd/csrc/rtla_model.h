@@ -1507,37 +1507,53 @@ RTLA_HD bool sym_twins(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, in
   }
   return same;
 }
-template <int NS, class RecF, class SlotF, class ElecF>
-RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of) {
+// A bag slot's share of its sender's / receiver's signature: the message
+// with both names dropped (msource /= mdest in every message), hashed.
+RTLA_HD uint32_t slot_sig_sent(const Layout& L, uint64_t v) {
+  const uint64_t sm = (1ull << L.b_sid) - 1ull;
+  const uint64_t anon = v & ~(sm << 2 | sm << (2 + L.b_sid));
+  return mix32((uint32_t)anon ^ mix32((uint32_t)(anon >> 32) + 0x632be5abu));
+}
+RTLA_HD uint32_t slot_sig_recv(uint32_t sent) { return mix32(sent ^ 0x5bd1e995u); }
+RTLA_HD uint32_t slot_src(const Layout& L, uint64_t v) { return (uint32_t)(v >> 2 & ((1ull << L.b_sid) - 1ull)); }
+RTLA_HD uint32_t slot_dst(const Layout& L, uint64_t v) {
+  return (uint32_t)(v >> (2 + L.b_sid) & ((1ull << L.b_sid) - 1ull));
+}
+// Server i's signature from its parts: the local part (srv_sig, high half)
+// and the sums of slot_sig_sent / slot_sig_recv over the messages it sent /
+// is sent.
+RTLA_HD uint64_t sig_of(uint32_t local, uint32_t ms, uint32_t mr) {
+  return (uint64_t)local << 32 | mix32(ms ^ mix32(mr + 0x27d4eb2fu));
+}
+// The signature parts of a state: loc[i], ms[i], mr[i] per server.
+template <int NS, class RecF, class SlotF>
+RTLA_HD void sym_sig_parts(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, uint32_t* loc, uint32_t* ms,
+                           uint32_t* mr) {
   constexpr int SW = 3 + NS;
-  // signatures: local part (high half) | sent/received message multisets
-  uint32_t ms[NS], mr[NS];
-  uint64_t sig[NS];
 #pragma unroll
   for (int j = 0; j < NS; j++) ms[j] = mr[j] = 0;
   for (int q = 0; q < nmsg; q++) {
     const uint64_t v = slot_of(q);
     if (!v) continue;
-    const uint64_t sm = (1ull << L.b_sid) - 1ull;
-    const uint32_t src = (uint32_t)(v >> 2 & sm), dst = (uint32_t)(v >> (2 + L.b_sid) & sm);
-    const uint64_t anon = v & ~(sm << 2 | sm << (2 + L.b_sid));  // names dropped (msource /= mdest in every message)
-    const uint32_t c = mix32((uint32_t)anon ^ mix32((uint32_t)(anon >> 32) + 0x632be5abu));
-    const uint32_t cr = mix32(c ^ 0x5bd1e995u);
+    const uint32_t src = slot_src(L, v), dst = slot_dst(L, v);
+    const uint32_t c = slot_sig_sent(L, v), cr = slot_sig_recv(c);
 #pragma unroll
     for (int j = 0; j < NS; j++) {
       ms[j] += src == (uint32_t)j ? c : 0u;
       mr[j] += dst == (uint32_t)j ? cr : 0u;
     }
   }
-#pragma unroll
-  for (int j = 0; j < NS; j++) sig[j] = 0;
 #pragma unroll 1
   for (int i = 0; i < NS; i++) {  // one record live at a time
     uint32_t rec[SW];
     rec_of(i, rec);
-    const uint64_t si = (uint64_t)srv_sig<NS>(i, rec) << 32 | mix32(sel_word<NS>(ms, i) ^ mix32(sel_word<NS>(mr, i) + 0x27d4eb2fu));
-    set_at<NS>(sig, i, si);
+    set_at<NS>(loc, i, srv_sig<NS>(i, rec));
   }
+}
+// Ranking from the signatures: C(s)'s tie groups (and |C(s)|).
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD SymRank sym_rank_from(const Layout& L, const uint64_t* sig, RecF rec_of, int nmsg, SlotF slot_of, int nelec,
+                              ElecF elec_of) {
   // pi[i] ranges over [lo_i, lo_i + cnt_i); server i picks among the
   // positions its tie group has left: rad_i = cnt_i - (tied servers before i)
   SymRank r{0, 0, 0, 1};
@@ -1580,6 +1596,15 @@ RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, 
     for (int i = 0; i < NS; i++) r.ncomb *= (int)pk_get<NS>(r.radm, i);
   }
   return r;
+}
+template <int NS, class RecF, class SlotF, class ElecF>
+RTLA_HD SymRank sym_rank(const Layout& L, RecF rec_of, int nmsg, SlotF slot_of, int nelec, ElecF elec_of) {
+  uint32_t loc[NS], ms[NS], mr[NS];
+  sym_sig_parts<NS>(L, rec_of, nmsg, slot_of, loc, ms, mr);
+  uint64_t sig[NS];
+#pragma unroll
+  for (int i = 0; i < NS; i++) sig[i] = sig_of(loc[i], ms[i], mr[i]);
+  return sym_rank_from<NS>(L, sig, rec_of, nmsg, slot_of, nelec, elec_of);
 }
 // Fingerprint of pi_k(s), the k-th member (0 <= k < r.ncomb) of C(s).
 template <int NS, class RecF, class SlotF, class ElecF>

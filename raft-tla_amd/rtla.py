@@ -50,7 +50,8 @@ class _Cfg(C.Structure):
                 ("max_log", C.c_int32), ("max_copies", C.c_int32), ("max_msgs", C.c_int32),
                 ("bag_cap", C.c_int32), ("elec_cap", C.c_int32), ("inv_mask", C.c_int32),
                 ("symmetry", C.c_int32), ("fpset_log2", C.c_int32), ("shards", C.c_int32),
-                ("frontier_cap", C.c_uint64), ("mem_budget", C.c_uint64), ("chunk", C.c_uint64)]
+                ("frontier_cap", C.c_uint64), ("mem_budget", C.c_uint64), ("chunk", C.c_uint64),
+                ("mode", C.c_int32), ("reserved", C.c_int32)]
 
 
 class _Stats(C.Structure):
@@ -152,6 +153,7 @@ class Config:
     shards: int = 0
     chunk: int = 0
     symmetry: bool = False  # SYMMETRY Permutations(Server) (specs/MC.tla)
+    dedup_only: bool = False  # RTLA_MODE_DEDUP: the synthetic microbench's context (no BFS, no parent records)
 
     @property
     def inv_mask(self) -> int:
@@ -163,7 +165,8 @@ class Config:
     def c(self) -> _Cfg:
         return _Cfg(self.n_server, self.n_value, self.max_term, self.max_log, self.max_copies,
                     self.max_msgs, self.bag_cap, self.elec_cap, self.inv_mask, int(self.symmetry),
-                    self.fpset_log2, self.shards, self.frontier_cap, self.mem_budget, self.chunk)
+                    self.fpset_log2, self.shards, self.frontier_cap, self.mem_budget, self.chunk,
+                    1 if self.dedup_only else 0, 0)
 
 
 @dataclass

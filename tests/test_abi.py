@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 def test_python_mirror_binds_every_symbol():
     import rtla
     assert sorted(rtla.EXPORTED) == declared_symbols()
-    assert rtla._lib.rtla_abi_version() == 8
+    assert rtla._lib.rtla_abi_version() == 9
 
 
 def test_row_layout_and_config_errors():
