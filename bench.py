@@ -79,16 +79,20 @@ SECONDARY = "raft3_v2_t2_l2_m2"    # wall time to exhaust (the default run repor
 # (configs[1] 197.2 -> 192.1 ms, configs[0] 300.9 -> 291.1, configs[2] 90.0 ->
 # 88.4; 2^33: 194.9 ms, the clear grows faster; profiles/r04_v4/fpset_*.json).
 FPSET_LOG2 = {"raft3_v2_t2_l2_m2": 33, "raft3_v2_t2_l1_m3": 32, "raft3_v2_t2_l1_m2": 30,
-              "cfg2": 32, "cfg1": 32, "cfg3": 32, "cfg4": 30, "synthetic": 33}
+              "cfg2": 32, "cfg1": 32, "cfg3": 32, "cfg4": 30,
+              # 1e9 inputs with a 1e8 pool find ~8.6e9 distinct successor fingerprints: 2^34 slots
+              # (128 GiB, ~50 % load) on one GPU; N ranks each 1/N of the inputs in 2^34 / N
+              "synthetic": 34}
 # Bag slots per row for the unbounded-bag configs.  A state d BFS levels below
 # Init holds at most d - 1 distinct messages (every action adds at most one),
 # so this bounds the depth at which the row format -- not memory -- stops the
 # search; a successor that needs more raises RTLA_CAP_ROW, never truncates.
 BAG_CAP = {"cfg2": 18, "cfg1": 24, "cfg3": 20, "cfg4": 20, "synthetic": 12}
-# Synthetic microbench: input states per GPU (1e9 over 8 GPUs), the pool half
-# of them are redrawn from (so dedup has hits), states per device batch.
-SYNTH_STATES = 125_000_000
-SYNTH_POOL_FRAC = 10
+# Synthetic microbench: 1e9 input states over the whole job,
+# half of them redrawn from a pool of 1e8 (so dedup has hits); states
+# generated per device batch.
+SYNTH_TOTAL = 1_000_000_000
+SYNTH_POOL = 100_000_000
 SYNTH_BATCH = 1 << 24
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Pure-stream rates of random 8-byte fingerprint-set accesses into a 32 GiB
@@ -129,7 +133,8 @@ def fpset_log2_for(workload, world, override=0, shards=0, pinned=True):
     reaches deeper levels.  Virtual shards on one GPU (--shards S) split the
     single-GPU set S ways, as S ranks would."""
     fpl = override or FPSET_LOG2.get(workload, 30)
-    if not override and world > 1 and (workload not in CAPPED or pinned):
+    # (the synthetic microbench's ranks are replicas, each with its own set: its 2^34 slots stay per rank)
+    if not override and world > 1 and (workload not in CAPPED or pinned) and workload != "synthetic":
         fpl = max(24, fpl - (world - 1).bit_length())
     if not override and shards > 1:
         fpl = max(24, fpl - (shards - 1).bit_length())
@@ -227,10 +232,11 @@ def cpu_baseline(shape, sample_states, threads):
 
 def cpu_baseline_synthetic(rtla, cfg, pool, threads, target_s=12.0):
     """The synthetic microbench's CPU leg: the same random input states
-    (rtla_random_texts: the generator's rows printed as state text, outside
-    the timed region) parsed by the C oracle and run through Next + dedup
-    into one seen set (oracle/raft_cpu.c orc_dedup_texts) -- batches until
-    ~target_s seconds of oracle time."""
+    (rtla_random_texts: the generator's rows printed as state text) parsed by
+    the C oracle, then -- the timed phase -- run through Next + dedup into
+    one seen set (oracle/raft_cpu.c orc_dedup_texts; the parse is untimed, as
+    the GPU leg is handed packed rows) -- batches until ~target_s seconds of
+    timed oracle work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import raft_cpu
     n, v, t, l, c, m, inv = WORKLOADS["synthetic"]
@@ -261,7 +267,7 @@ class Run:
                                   pinned=args.depth == "pinned" and name in PINNED_LEVELS)
         self.cfg = rtla.Config(n, v, t, l, c, m, inv, fpset_log2=self.fpl, shards=args.shards,
                                bag_cap=BAG_CAP.get(name, 0), frontier_cap=frontier_cap,
-                               symmetry=name in SYMMETRIC,
+                               symmetry=name in SYMMETRIC, dedup_only=name == "synthetic",
                                mem_budget=(args.mem_budget << 30) if args.mem_budget else
                                (200 << 30) if args.shards > 1 else 0, chunk=args.chunk)
         self.ck = rtla.Checker(self.cfg, rank=rank, world=world, comm_id=comm_id)
@@ -416,34 +422,56 @@ def capacity(levels, info, fpl, parts=1):
 
 
 def synthetic(run, args, rank, world, barrier):
-    """BASELINE configs[4]: the rank's input states are generated on the
-    device once, before any timing (batches of SYNTH_BATCH into the row
-    arena: inputs resident in HBM); a step = every input state through Next
-    + fingerprint + dedup (one level-kernel launch over the resident rows)
-    into the rank's fingerprint set, cleared first.  Each rank takes its own
-    range of the input numbering; with several ranks each deduplicates what
-    it generates (independent replicas: no exchange)."""
-    n = args.synth_states
-    pool = n // SYNTH_POOL_FRAC
+    """BASELINE configs[4]: 1e9 input states over the job,
+    each rank its own 1/N of the input numbering (input i is state
+    synth_state_id(i): half of them redrawn from the job-wide 1e8 pool).  A
+    step clears the rank's fingerprint set and runs every input through Next
+    + fingerprint + dedup (level-kernel launches in dedup-only mode) into it.
+    The inputs are generated on the device into the row arena in passes of
+    as many rows as it holds (at N = 1 the 1e9 x 252 B do not fit HBM beside
+    the set): each pass is generated OUTSIDE the timed region (a single pass
+    once, before all steps), so every timed dedup runs over HBM-resident rows.
+    With several ranks each deduplicates its own inputs (replicas: no
+    exchange; 'parallelism' says so)."""
+    n = args.synth_states // world
     first0 = rank * n
-    for b in range(0, n, SYNTH_BATCH):
-        run.ck.synthetic_generate(first0 + b, min(SYNTH_BATCH, n - b), pool, at=b)
+    rows = int(json.loads(run.ck.device_info())["frontier_cap"])
+    per = min(n, rows) // 64 * 64
+    passes = [(b, min(per, n - b)) for b in range(0, n, per)]
+
+    def generate(b, m):
+        for g in range(0, m, SYNTH_BATCH):
+            run.ck.synthetic_generate(first0 + b + g, min(SYNTH_BATCH, m - g), args.synth_pool, at=g)
+
+    if len(passes) == 1:
+        generate(*passes[0])
 
     def one():
+        t = time.perf_counter()
         run.ck.reset()
-        lv = run.ck.synthetic_dedup(0, n)
-        return {"generated": lv.generated, "probes": lv.probes, "new": lv.new, "kernel_ms": lv.kernel_ms,
-                "batches": 1}
+        timed_s = time.perf_counter() - t
+        tot = {"generated": 0, "probes": 0, "new": 0, "kernel_ms": 0.0, "batches": len(passes)}
+        for b, m in passes:
+            if len(passes) > 1:
+                generate(b, m)  # (untimed)
+            t = time.perf_counter()
+            lv = run.ck.synthetic_dedup(0, m)
+            timed_s += time.perf_counter() - t
+            tot["generated"] += lv.generated
+            tot["probes"] += lv.probes
+            tot["new"] += lv.new
+            tot["kernel_ms"] += lv.kernel_ms
+        return timed_s, tot
 
     for _ in range(args.warmup):
         one()
     barrier()
-    t0 = time.perf_counter()
+    timed = 0.0
     for _ in range(args.steps):
-        tot = one()
-    t1 = time.perf_counter()
+        dt, tot = one()
+        timed += dt
     barrier()
-    return max_over_ranks(t1 - t0, world) / args.steps, tot, pool
+    return max_over_ranks(timed, world) / args.steps, tot, n, per
 
 
 def print_levels(name, levels):
@@ -471,8 +499,10 @@ def main():
                     help="device memory per rank in GiB (0 = 85 %% of what is free; several ranks sharing one GPU, "
                          "e.g. over RTLA_TRANSPORT=shm, need a share each)")
     ap.add_argument("--levels", action="store_true", help="print the per-level tables to stderr")
-    ap.add_argument("--synth-states", type=int, default=SYNTH_STATES,
-                    help="synthetic workload: input states per GPU")
+    ap.add_argument("--synth-states", type=int, default=SYNTH_TOTAL,
+                    help="synthetic workload: input states of the whole job (split over the ranks)")
+    ap.add_argument("--synth-pool", type=int, default=SYNTH_POOL,
+                    help="synthetic workload: half the inputs are redrawn from a pool of this many states")
     ap.add_argument("--depth", choices=("pinned", "fit"), default="pinned",
                     help="capped workloads: the oracle-pinned levels (default), or as many as device memory holds")
     ap.add_argument("--cap-levels", type=int, default=0,
@@ -525,9 +555,9 @@ def main():
     run = Run(rtla, args.workload, rank, world, comm_id, args, args.frontier_cap)
     info = json.loads(run.ck.device_info())
     if args.workload == "synthetic":
-        per_step, tot, pool = synthetic(run, args, rank, world, barrier)
+        per_step, tot, n, per = synthetic(run, args, rank, world, barrier)
+        pool = args.synth_pool
         S = run.ck.levels[0].row_bytes if run.ck.levels else 4 * rtla.row_words(run.cfg)
-        n = args.synth_states
         ems = tot["kernel_ms"]
         P, D = tot["probes"], tot["new"]
         kbytes = n * S + P * 64
@@ -538,16 +568,25 @@ def main():
         out = {
             "metric": "random packed states/sec through Next + fingerprint + dedup (BASELINE configs[4])",
             "value": n * world / per_step, "unit": "input states/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": per_step * 1e3, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": per_step * 1e3, "higher_is_better": True,
+            "scaling": "strong",  # 1e9 inputs over the job at every N
             "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: counter-based PRNG (seed 0x5AF72025) valid random states, 1/2 redrawn from a pool",
+            "data": "synthetic: counter-based PRNG (seed 0x5AF72025) valid random states, 1/2 redrawn from a "
+                    "job-wide pool of %d" % pool,
             "config": {"workload": "synthetic", "baseline_config": 4, "layout": "cfg-3: N3 V2 T4 L3 C2, bag_cap 12",
-                       "input_states_per_gpu": n, "pool": pool, "inputs": "generated once, resident in HBM",
+                       "input_states": n * world, "input_states_per_gpu": n, "pool": pool,
+                       "resident_rows_per_pass": per, "passes_per_step": tot["batches"],
+                       "inputs": ("generated once before the timed steps, resident in HBM" if tot["batches"] == 1 else
+                                  "generated on the device into the row arena before each dedup pass, outside the "
+                                  "timed region (%d x %d B do not fit HBM beside the set): every timed pass runs "
+                                  "over resident rows" % (n, S)),
+                       "timed": "per step: the fingerprint-set clear + every dedup pass",
                        "launches_per_step": tot["batches"],
                        "generated": tot["generated"], "probes": P, "distinct_successors": D,
                        "successors_per_s": tot["generated"] * world / per_step, "row_bytes": S,
-                       "fpset_slots_log2": run.fpl,
-                       "parallelism": "single" if world == 1 else "replicas%d" % world},
+                       "fpset_slots_log2": run.fpl, "fpset_load": D / float(1 << run.fpl),
+                       "parallelism": "single" if world == 1 else
+                       "replicas%d (each rank deduplicates its own 1/N of the inputs; no exchange)" % world},
             "roofline": {"bound": "hbm", "achieved": kbytes / (ems / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": kbytes / (ems / 1e3) / 1e9 / HBM_PEAK_GBS,
                          "traffic": straffic["bytes_per_launch"] if straffic else None,

@@ -14,26 +14,33 @@ using namespace rtla;
 
 // Owner side of the exchange: insert the fingerprints other shards sent and
 // answer each record with 1 (new: the sender builds the state) or 0 (seen).
-// Region p (grid.y) holds counts[p] records.  Each thread takes IR records a
+// Region p holds counts[p] records.  Record slot t of the launch is record
+// t / nshard of region t % nshard: the sources interleave, so when several
+// senders queued the same new fingerprint in one round, which one wins (and
+// builds its row) is not biased towards low shard ids -- the shards' next
+// levels stay even without re-balancing.  Each thread takes IR slots a
 // stride apart and issues their home-slot loads together (IR random reads
-// in flight per lane); no per-wave atomics (the two-phase exchange needs no
-// dense ranks).
+// in flight per lane).
 constexpr int IR = 4;
 __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
                                 const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
-                                unsigned long long* table, int tlog2, uint32_t* __restrict__ ans, DevCounters* ctr) {
-  const unsigned long long p = blockIdx.y;
-  const unsigned long long n = counts[p];
+                                unsigned long long max_count, unsigned long long* table, int tlog2,
+                                uint32_t* __restrict__ ans, DevCounters* ctr) {
   const int lane = threadIdx.x & 63;
   unsigned probes = 0;
+  const unsigned long long total = max_count * (unsigned long long)nshard;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long k0 = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k0 < n; k0 += IR * stride) {
+  for (unsigned long long t0 = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; t0 < total;
+       t0 += IR * stride) {
     FP f[IR];
+    unsigned long long at[IR];  // p * cap + k, or ~0 (no record)
     unsigned long long seen[IR];
 #pragma unroll
     for (int u = 0; u < IR; u++) {
-      const unsigned long long k = k0 + u * stride;
-      f[u] = k < n ? FP{recv_fp[2 * (p * cap + k)], recv_fp[2 * (p * cap + k) + 1]} : FP{0, 0};
+      const unsigned long long t = t0 + u * stride;
+      const unsigned long long p = t % (unsigned long long)nshard, k = t / (unsigned long long)nshard;
+      at[u] = t < total && k < counts[p] ? p * cap + k : ~0ull;
+      f[u] = at[u] != ~0ull ? FP{recv_fp[2 * at[u]], recv_fp[2 * at[u] + 1]} : FP{0, 0};
     }
 #pragma unroll
     for (int u = 0; u < IR; u++)  // load first (the owner may know the state: a load is cheaper than an atomic)
@@ -42,14 +49,13 @@ __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
                                   : 0ull;
 #pragma unroll
     for (int u = 0; u < IR; u++) {
-      const unsigned long long k = k0 + u * stride;
-      if (k >= n) continue;
+      if (at[u] == ~0ull) continue;
       uint32_t r = 0;
       if (f[u].a | f[u].b) {  // 0:0 = a hole in the sender's outbox chunk
         r = fpset_resolve_loaded(table, tlog2, f[u].b | 1ull, f[u].a >> (64 - tlog2), seen[u], ctr) ? 1u : 0u;
         probes++;
       }
-      ans[p * cap + k] = r;
+      ans[at[u]] = r;
     }
   }
   for (int off = 32; off > 0; off >>= 1) probes += __shfl_down(probes, off);
@@ -356,9 +362,10 @@ hipError_t launch_insert_remote(const uint64_t* recv_fp, const uint64_t* counts,
                                 uint64_t* table, int tlog2, uint32_t* ans, DevCounters* ctr, uint64_t max_count,
                                 hipStream_t st) {
   if (!max_count) return hipSuccess;
-  hipLaunchKernelGGL(k_insert_remote, dim3(grid_x((max_count + IR - 1) / IR, 256), nshard), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_insert_remote, dim3(grid_x((max_count * nshard + IR - 1) / IR, 256)), dim3(256), 0, st,
                      (const unsigned long long*)recv_fp, (const unsigned long long*)counts, nshard,
-                     (unsigned long long)cap, (unsigned long long*)table, tlog2, ans, ctr);
+                     (unsigned long long)cap, (unsigned long long)max_count, (unsigned long long*)table, tlog2, ans,
+                     ctr);
   return hipGetLastError();
 }
 

@@ -549,6 +549,9 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
 // row differs from the parent's copy (child_write; `wait`: the copies must
 // land first).  NOT inlined for the same reason as key_one: at the SYMMETRY
 // kernel's 128 VGPRs the inlined build pass is one of the two big spillers.
+#ifndef RTLA_BUILD_SORT
+#define RTLA_BUILD_SORT 1  // build_all: new states ordered by family (batches of 64 diverge over fewer families)
+#endif
 #ifndef RTLA_SYM_BUILD_CALL
 #define RTLA_SYM_BUILD_CALL 1
 #endif
@@ -728,9 +731,58 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   //      which its child differs from the parent (child_write, rtla_model.h).
   // No separate row-building kernel: no parent-record read, no parent-row
   // gather, no second launch.
+  // compute_delta over a chunk of lanes, specialised for its family when the
+  // whole chunk holds one (D = DeltaFpT for the probe pass, DeltaT for the
+  // row build and orbit keys)
+  auto chunk_delta = [&](bool active, const uint32_t* prow, int inst, auto& d) {
+    const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
+    const bool one_family = __ballot(active && inst_family(L, inst) != f0) == 0ull;
+    if (!one_family || (xflags & XF_GENERIC_DELTA)) {
+      if (active) compute_delta<NS>(L, prow, inst, d);
+    } else if (active) {
+      switch (f0) {  // one family in the whole chunk: its code only
+        case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
+        case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
+        case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
+        case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
+        case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
+        case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
+        case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
+        case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
+        case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
+        default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
+      }
+    }
+  };
   auto build_all = [&]() {
     const int ntot = tail - head;  // uniform
     if (ntot == 0) return;
+    if (RTLA_BUILD_SORT && ntot > 64 && ntot <= 8 * 64) {
+      // order the pending new states by action family (a stable counting
+      // sort, through registers): each batch of 64 below then spans few
+      // families, so its lanes' compute_delta diverges over fewer of the
+      // families' code paths
+      uint32_t ev[8];
+      int fm[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int idx = j * 64 + lane;
+        const bool a = idx < ntot;
+        ev[j] = a ? newl[(head + idx) & (NEWCAP - 1)] : 0u;
+        fm[j] = a ? inst_family(L, (int)(ev[j] & 255u)) : F_COUNT;
+      }
+      int base = 0;
+      for (int f = 0; f < F_COUNT; f++) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          if (j * 64 >= ntot) break;
+          const unsigned long long m = __ballot(fm[j] == f);
+          if (fm[j] == f) newl[(head + base + __popcll(m & lanes_below)) & (NEWCAP - 1)] = (uint16_t)ev[j];
+          base += __popcll(m);
+        }
+      }
+      wave_sync();
+    }
     unsigned long long obase = 0;
     if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)ntot);
     obase = shfl0_u64(obase);
@@ -990,28 +1042,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   FP ncf{0, 0};
   int nowner = me;
   uint32_t ninfo_new = 0;
-  // compute_delta over a chunk, specialised for its family when the whole
-  // chunk holds one (D = DeltaFpT for the probe pass, DeltaT for orbit keys)
-  auto chunk_delta = [&](bool active, const uint32_t* prow, int inst, auto& d) {
-    const int f0 = inst_family(L, __builtin_amdgcn_readfirstlane(inst));
-    const bool one_family = __ballot(active && inst_family(L, inst) != f0) == 0ull;
-    if (!one_family || (xflags & XF_GENERIC_DELTA)) {
-      if (active) compute_delta<NS>(L, prow, inst, d);
-    } else if (active) {
-      switch (f0) {  // one family in the whole chunk: its code only
-        case F_RESTART: compute_delta<NS, F_RESTART>(L, prow, inst, d); break;
-        case F_TIMEOUT: compute_delta<NS, F_TIMEOUT>(L, prow, inst, d); break;
-        case F_REQUESTVOTE: compute_delta<NS, F_REQUESTVOTE>(L, prow, inst, d); break;
-        case F_BECOMELEADER: compute_delta<NS, F_BECOMELEADER>(L, prow, inst, d); break;
-        case F_CLIENTREQUEST: compute_delta<NS, F_CLIENTREQUEST>(L, prow, inst, d); break;
-        case F_ADVANCECOMMIT: compute_delta<NS, F_ADVANCECOMMIT>(L, prow, inst, d); break;
-        case F_APPENDENTRIES: compute_delta<NS, F_APPENDENTRIES>(L, prow, inst, d); break;
-        case F_RECEIVE: compute_delta<NS, F_RECEIVE>(L, prow, inst, d); break;
-        case F_DUPLICATE: compute_delta<NS, F_DUPLICATE>(L, prow, inst, d); break;
-        default: compute_delta<NS, F_DROP>(L, prow, inst, d); break;
-      }
-    }
-  };
   auto eval_chunk = [&](int done, int cnt) {
     const bool active = lane < cnt;
     const int e = active ? ring[(done + lane) & (RING - 1)] : 0;
@@ -1390,8 +1420,11 @@ constexpr int compact_group(const Layout& L) {
 #ifndef RTLA_GROUP32_LDS
 #define RTLA_GROUP32_LDS (19 * 1024)
 #endif
+#ifndef RTLA_SYM_GROUP
+#define RTLA_SYM_GROUP 16
+#endif
 constexpr int spec_group(const Layout& L) {
-  if (L.sym) return 16;  // configs[3]: 16 waves/CU at 128 VGPRs need the smaller tile (311.5 vs 322 ms)
+  if (L.sym) return RTLA_SYM_GROUP;  // configs[3]: 16 waves/CU at 128 VGPRs need the smaller tile (311.5 vs 322 ms)
   const int g = compact_group(L);
   return g == 32 && compact_lds_words(L.W, L.all_words, 32, L.sym, true) * sizeof(uint32_t) > RTLA_GROUP32_LDS ? 16 : g;
 }
