@@ -21,7 +21,10 @@ using namespace rtla;
 // levels stay even without re-balancing.  Each thread takes IR slots a
 // stride apart and issues their home-slot loads together (IR random reads
 // in flight per lane).
-constexpr int IR = 4;
+#ifndef RTLA_INSERT_IR
+#define RTLA_INSERT_IR 4
+#endif
+constexpr int IR = RTLA_INSERT_IR;
 __global__ void k_insert_remote(const unsigned long long* __restrict__ recv_fp,
                                 const unsigned long long* __restrict__ counts, int nshard, unsigned long long cap,
                                 unsigned long long max_count, unsigned long long* table, int tlog2,

@@ -549,9 +549,6 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
 // row differs from the parent's copy (child_write; `wait`: the copies must
 // land first).  NOT inlined for the same reason as key_one: at the SYMMETRY
 // kernel's 128 VGPRs the inlined build pass is one of the two big spillers.
-#ifndef RTLA_BUILD_SORT
-#define RTLA_BUILD_SORT 1  // build_all: new states ordered by family (batches of 64 diverge over fewer families)
-#endif
 #ifndef RTLA_SYM_BUILD_CALL
 #define RTLA_SYM_BUILD_CALL 1
 #endif
@@ -757,32 +754,6 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
   auto build_all = [&]() {
     const int ntot = tail - head;  // uniform
     if (ntot == 0) return;
-    if (RTLA_BUILD_SORT && ntot > 64 && ntot <= 8 * 64) {
-      // order the pending new states by action family (a stable counting
-      // sort, through registers): each batch of 64 below then spans few
-      // families, so its lanes' compute_delta diverges over fewer of the
-      // families' code paths
-      uint32_t ev[8];
-      int fm[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int idx = j * 64 + lane;
-        const bool a = idx < ntot;
-        ev[j] = a ? newl[(head + idx) & (NEWCAP - 1)] : 0u;
-        fm[j] = a ? inst_family(L, (int)(ev[j] & 255u)) : F_COUNT;
-      }
-      int base = 0;
-      for (int f = 0; f < F_COUNT; f++) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          if (j * 64 >= ntot) break;
-          const unsigned long long m = __ballot(fm[j] == f);
-          if (fm[j] == f) newl[(head + base + __popcll(m & lanes_below)) & (NEWCAP - 1)] = (uint16_t)ev[j];
-          base += __popcll(m);
-        }
-      }
-      wave_sync();
-    }
     unsigned long long obase = 0;
     if (lane == 0) obase = atomicAdd(&ctr->next_count, (unsigned long long)ntot);
     obase = shfl0_u64(obase);
