@@ -13,7 +13,7 @@
 // frontiers are (rtla_step re-balances what drifts).  Invariants and
 // distinct coverage are evaluated here, where parent and action are known.
 // LC: compiled-in layout (Layout{} = run-time Lrt), as for the level kernel.
-constexpr int BW_QUEUE = 512;  // per-wave LDS queue of winner refs (u64): sorted by family, built 64 at a time
+constexpr int BW_QUEUE = 128;  // per-wave LDS queue of winner refs (u64): batches of 64 winners
 __host__ __device__ constexpr int build_winners_lds_words(int W, int AW) {
   return lane_lds_words(W, AW) + 2 * BW_QUEUE;
 }
@@ -25,14 +25,12 @@ k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
                 unsigned long long* __restrict__ parents, unsigned long long next_base, unsigned long long next_cap,
                 DevCounters* ctr) {
   // A wave scans 64 records of owner p (grid.y) at a time and queues the
-  // winners' refs in LDS; once 448 are queued (and at the end) it orders the
-  // queue by action family and builds it 64 winners -- one full wave -- at a
-  // time: gathers their parent rows into LDS (one coalesced read per row),
-  // builds each successor in place, reserves next-level slots with one
-  // atomic and stores the rows (one coalesced write per row) and parent
-  // records.  (A batch per 64 records instead would run compute_delta on the
-  // ~quarter of the lanes whose record won; a batch in record order mixes
-  // most of the families, whose code paths its lanes then take in turn.)
+  // winners' refs in LDS; every 64 queued winners -- one full wave -- it
+  // gathers their parent rows into LDS (one coalesced read per row), builds
+  // each successor in place, reserves next-level slots with one atomic and
+  // stores the rows (one coalesced write per row) and parent records.  (A
+  // batch per 64 records instead would run compute_delta on the ~quarter of
+  // the lanes whose record won.)
   const Layout& L = pick_layout<LC>(Lrt);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ unsigned int cov[COVER_CODES];
@@ -84,50 +82,6 @@ k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
   };
   int qn = 0;  // winners queued (wave-uniform)
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
-  // stable counting sort of q[0, qn) by action family, through registers
-  auto sort_queue = [&]() {
-    unsigned long long ev[BW_QUEUE / 64];
-    int fm[BW_QUEUE / 64];
-#pragma unroll
-    for (int j = 0; j < BW_QUEUE / 64; j++) {
-      const int idx = j * 64 + lane;
-      ev[j] = idx < qn ? q[idx] : 0ull;
-      fm[j] = idx < qn ? inst_family(L, (int)(ev[j] & 0xffffull)) : F_COUNT;
-    }
-    wave_sync();
-    int base = 0;
-    for (int f = 0; f < F_COUNT; f++) {
-#pragma unroll
-      for (int j = 0; j < BW_QUEUE / 64; j++) {
-        const unsigned long long m = __ballot(fm[j] == f);
-        if (fm[j] == f) q[base + __popcll(m & lanes_below)] = ev[j];
-        base += __popcll(m);
-      }
-    }
-    wave_sync();
-  };
-  // build the queued winners 64 at a time (all of them when `all`), the rest to the front
-  auto drain_queue = [&](bool all) {
-    sort_queue();
-    int at = 0;
-    for (; qn - at >= 64; at += 64) {
-      if (at) {
-        if (lane < 64) q[lane] = q[at + lane];  // (build reads q[0, 64))
-        wave_sync();
-      }
-      build(64);
-    }
-    const int rest = qn - at;
-    if (at && rest) {
-      if (lane < rest) q[lane] = q[at + lane];
-      wave_sync();
-    }
-    qn = rest;
-    if (all && qn) {
-      build(qn);
-      qn = 0;
-    }
-  };
   for (unsigned long long k0 = ((unsigned long long)blockIdx.x * wpb + wave) * 64ull; k0 < n;
        k0 += (unsigned long long)gridDim.x * wpb * 64ull) {
     const unsigned long long k = k0 + lane;
@@ -136,9 +90,14 @@ k_build_winners(Layout Lrt, Ring cur, unsigned long long cur_base, int me,
     if (win) q[qn + __popcll(m & lanes_below)] = send_ref[p * cap + k];
     qn += __popcll(m);
     wave_sync();
-    if (qn > BW_QUEUE - 64) drain_queue(false);
+    if (qn >= 64) {
+      build(64);
+      qn -= 64;
+      if (lane < qn) q[lane] = q[64 + lane];  // (the rest moves to the front: fewer than 64)
+      wave_sync();
+    }
   }
-  drain_queue(true);
+  if (qn) build(qn);
   __syncthreads();
   for (int k = threadIdx.x; k < COVER_CODES; k += blockDim.x)
     if (cov[k]) atomicAdd(&ctr->cover[COVER_CODES + k], (unsigned long long)cov[k]);
