@@ -549,9 +549,6 @@ __device__ __noinline__ KeyStep key_one(const Layout& Lrt, const uint32_t* prow,
 // row differs from the parent's copy (child_write; `wait`: the copies must
 // land first).  NOT inlined for the same reason as key_one: at the SYMMETRY
 // kernel's 128 VGPRs the inlined build pass is one of the two big spillers.
-#ifndef RTLA_RESOLVE_LOAD_FIRST
-#define RTLA_RESOLVE_LOAD_FIRST 1  // a pipelined CAS that found another key continues load-first (CAS only empty slots)
-#endif
 #ifndef RTLA_SYM_BUILD_CALL
 #define RTLA_SYM_BUILD_CALL 1
 #endif
@@ -899,16 +896,8 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     } else if (async_cas) {
       if (cflight) {  // the CAS issued one chunk ago
         if (cold == 0ull) isnew = true;
-        else if (cold != ckey) {  // rare: keep probing, load-first (the set only: a sent-cache store reports 0)
-#if RTLA_RESOLVE_LOAD_FIRST
-          const unsigned long long nidx = (cidx + 1ull) & ((1ull << tlog2) - 1ull);
-          isnew = fpset_resolve_loaded(table, tlog2, ckey, nidx,
-                                       __hip_atomic_load(&table[nidx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                       ctr);
-#else
+        else if (cold != ckey)  // rare: keep probing (the set only: a sent-cache store reports 0)
           isnew = fpset_resolve(table, tlog2, ckey, cidx, cold, ctr);
-#endif
-        }
       }
       ninfo = cinfo;
       nf = cf;
