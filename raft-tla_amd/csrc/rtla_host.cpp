@@ -1556,6 +1556,7 @@ static void print_stamps(const DevCounters& c, int level) {
   if (c.cas) fprintf(stderr, "cas level %d: %llu pipelined CAS, %llu probes, %llu new\n", level,
                      (unsigned long long)c.cas, (unsigned long long)c.probes, (unsigned long long)c.next_count);
   static const char* ph[8] = {"group", "ring", "compute", "resolve", "issue", "rows", "drain", "keys+end"};
+  // (non-symmetric kernels: "drain" = the group-end row build, "keys+end" = the group-end probe drain)
   unsigned long long tot = 0;
   for (int k = 0; k < 8; k++) tot += c.stamp[k];
   if (!tot) return;

@@ -1328,6 +1328,7 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
       pfb = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     drain();
+    if constexpr (!KSPLIT) STAMP(7);  // (non-symmetric builds: slot 7 = the group-end probe drain alone)
     build_all();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("" ::"v"(pfa), "v"(pfb));

@@ -13,6 +13,6 @@ for path in sys.argv[1:]:
         m = re.match(r"stamps level (\d+): (.*) \(([\d.e+]+) wave-cycles\)", line)
         c = float(m.group(3))
         allc += c
-        for k, v in re.findall(r"(\w+) ([\d.]+)", m.group(2)):
+        for k, v in re.findall(r"([\w+]+) ([\d.]+)", m.group(2)):
             tot[k] = tot.get(k, 0.0) + float(v) * c
     print(path, " ".join("%s %.3f" % (k, v / allc) for k, v in tot.items()), "%.3g wave-cycles" % allc)
