@@ -933,6 +933,8 @@ static int size_exchange(rtla_ctx* x, uint64_t per) {
   // re-balancing staging: ~1/20 of the budget; more rows move in sub-rounds
   x->rows_cap = (per / 20) / (2ull * G * (L.W + 2) * 4);
   x->rows_cap = std::min<uint64_t>(std::max<uint64_t>(x->rows_cap, 256), x->box_cap);
+  if (const char* e = getenv("RTLA_ROWS_CAP"))  // tests: tiny staging, every re-balancing move in sub-rounds
+    if (atoll(e) > 0) x->rows_cap = std::min<uint64_t>((uint64_t)atoll(e), x->box_cap);
   if (x->world > 1) {  // min over the ranks (max of the complements); the overflow bound: max
     uint64_t v[5] = {~x->box_cap, ~(x->chunk ? x->chunk : ~0ull), ~x->rows_cap, x->over_cap, x->guarded ? 0ull : 1ull};
     if (int rc = allreduce_u64(x, v, 5, 1)) return rc;

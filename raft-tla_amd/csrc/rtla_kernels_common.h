@@ -430,8 +430,10 @@ __device__ __forceinline__ unsigned long long win_bits(unsigned long long bits, 
 
 // Instances [wb, wb+64) whose enabling guard holds in `row`.  A superset is
 // safe (compute_delta re-checks every guard); a subset would lose states.
+// dup = false: without DuplicateMessage (counted apart, see dup_counted).
 template <int NS>
-__device__ __forceinline__ unsigned long long cand_mask(const Layout& L, const uint32_t* row, int nmsg, int wb) {
+__device__ __forceinline__ unsigned long long cand_mask(const Layout& L, const uint32_t* row, int nmsg, int wb,
+                                                        bool dup = true) {
   constexpr int N = NS;
   unsigned long long rv = 0, bl = 0, ldr = 0, tmo = 0;
 #pragma unroll
@@ -462,7 +464,7 @@ __device__ __forceinline__ unsigned long long cand_mask(const Layout& L, const u
   m |= win_bits(ldr, L.fam[F_ADVANCECOMMIT] - wb);
   m |= win_bits(ae, L.fam[F_APPENDENTRIES] - wb);
   m |= win_bits(bag, L.fam[F_RECEIVE] - wb);
-  m |= win_bits(bag, L.fam[F_DUPLICATE] - wb);
+  if (dup) m |= win_bits(bag, L.fam[F_DUPLICATE] - wb);
   m |= win_bits(bag, L.fam[F_DROP] - wb);
   return m;
 }
@@ -497,6 +499,12 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 #ifndef RTLA_SYM_WAVES_PER_EU
 #define RTLA_SYM_WAVES_PER_EU 4      // SYMMETRY, the key pass a call of its own (key_one): 128 VGPRs (configs[3]:
                                      // 311.5 ms, 16-state groups) beat 168 (343 ms) and 102 (414 ms)
+#endif
+#ifndef RTLA_DUP_COUNTED
+#define RTLA_DUP_COUNTED 1  // 0: evaluate every DuplicateMessage successor (A/B builds)
+#endif
+#ifndef RTLA_DUP_NARROW
+#define RTLA_DUP_NARROW 0   // 1: count them in the narrow-row kernels too (A/B builds)
 #endif
 #ifndef RTLA_MULTI_ASYNC
 #define RTLA_MULTI_ASYNC 1  // multi-shard kernels pipeline their CAS too
@@ -677,6 +685,12 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
 #endif
   const int ninst = L.fam[F_COUNT];
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
+  // DuplicateMessage successors counted, not evaluated (see the group loop)
+  // (not in the narrow-row kernels at 4 waves/SIMD: the exhaust model's spills
+  // grow 39 -> 58 VGPRs with it and its run slows 1156 -> 1320 ms)
+  constexpr bool narrow = !SYM && LC.N != 0 && LC.W <= RTLA_NARROW_W;
+  const bool dup_counted = RTLA_DUP_COUNTED && (!narrow || RTLA_DUP_NARROW) && L.C == 1 &&
+                           !(xflags & (XF_ALL_SUCCESSORS | XF_NO_CHUNKS));
   RTLA_STAMP_DECL
   // pending probe (issued by the previous chunk).  MULTI: a successor owned
   // by another shard probes this shard's SENT cache instead of the set --
@@ -1247,8 +1261,25 @@ k_expand_compact(Layout Lrt, Ring cur, unsigned long long s_begin, unsigned long
     }
     wave_sync();
     STAMP(0);  // group start: work-queue atomic, row tile load, per-state setup
+    // With at most one copy of a message allowed (max copies 1), every
+    // DuplicateMessage successor (raft.tla:443-445) is out of the model: its
+    // one message's count becomes 2 (specs/MC.tla).  It differs from its
+    // parent in the bag alone, so the invariants -- which read servers and
+    // elections only -- hold on it as on the parent (every expanded state
+    // passed them, or the run stopped at its level).  Such successors are
+    // counted (generated, per-action coverage: one per message of the bag),
+    // not evaluated -- 1/6 of configs[1]'s successors.  The successor walks
+    // (XF_ALL_SUCCESSORS) still list them.
+    if (dup_counted) {
+      if (valid) my_gen += (unsigned)nmsg;
+      if (!(xflags & XF_NO_COVER)) {
+        int nd = valid ? nmsg : 0;
+        for (int off = 32; off > 0; off >>= 1) nd += __shfl_down(nd, off);
+        if (lane == 0 && nd) atomicAdd(&cov[F_DUPLICATE], (unsigned)nd);
+      }
+    }
     for (int wb = 0; wb < ((xflags & XF_NO_CHUNKS) ? 0 : ninst); wb += 64) {
-      const unsigned long long mask = valid ? cand_mask<NS>(L, prow_mine, nmsg, wb) : 0ull;
+      const unsigned long long mask = valid ? cand_mask<NS>(L, prow_mine, nmsg, wb, !dup_counted) : 0ull;
       unsigned long long todo = wave_or_u64(mask);
       int pos = 0, done = 0;
       while (todo || pos > done) {

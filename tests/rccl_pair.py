@@ -30,8 +30,11 @@ def main():
             time.sleep(0.05)
         cid = open(idfile, "rb").read()
     log2 = max(16, (int(g["distinct"] * 2)).bit_length())
+    # RCCL_PAIR_BUDGET_STEP: rank r gets r * STEP more bytes (ranks whose own
+    # sizing differs must still agree on the exchange sizes)
+    budget = (8 << log2) * 3 + (1 << 29) + rank * int(os.environ.get("RCCL_PAIR_BUDGET_STEP", "0"))
     cfg = rtla.Config(g["n_server"], g["n_value"], g["max_term"], g["max_log"], g["max_copies"], g["max_msgs"],
-                      tuple(g["invariants"]), fpset_log2=log2, mem_budget=(8 << log2) * 3 + (1 << 29),
+                      tuple(g["invariants"]), fpset_log2=log2, mem_budget=budget,
                       symmetry=bool(g.get("symmetry", False)), chunk=int(os.environ.get("RCCL_PAIR_CHUNK", "0")))
     levels = []
     if os.environ.get("RCCL_PAIR_MODE") == "recover_missing":

@@ -863,7 +863,36 @@ def test_ranks_over_shm_transport_match_golden(tmp_path, name, world):
         assert outs[0]["trace"] == outs[1]["trace"]
 
 
-def test_ranks_recover_fails_on_every_rank(tmp_path):
+def test_ranks_with_different_budgets_agree_on_exchange_sizes(tmp_path):
+    """Ranks whose own sizing differs (different memory budgets, and a
+    re-balancing staging of 16 rows on rank 0 against 40 on rank 1) agree on
+    one set of exchange sizes in rtla_open (min over the ranks), so the
+    level-end re-balancing moves -- here many times the staging, in
+    sub-rounds -- post matching sends and receives: golden counts on every
+    rank, no hang (rows_cap from each rank's own budget)."""
+    import subprocess
+    import sys
+    name, world = "n3_v1_t2_l1_m1", 2
+    g = GOLD[name]
+    idfile = str(tmp_path / "comm_id")
+    helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_pair.py")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RTLA_TRANSPORT="shm", RTLA_SHM_SLOT_MB="32", RTLA_ROWS_CAP=str(16 + 24 * r),
+                   RCCL_PAIR_BUDGET_STEP=str(3 << 28))
+        procs.append(subprocess.Popen([sys.executable, helper, str(r), str(world), idfile, name], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-2000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    moved = 0
+    for o in outs:
+        assert o["levels"] == g["levels"], "rank %d" % o["rank"]
+        assert (o["distinct"], o["generated"]) == (g["distinct"], g["generated"])
+        moved += json.loads(o["info"])["rebalanced_rows"]
+    assert moved > 4 * 16  # the re-balancing ran, in several sub-rounds of the agreed 16 rows
     """One rank's checkpoint file is missing: rtla_recover fails on EVERY rank
     and returns promptly -- the local failure travels in the cross-rank
     consistency reduction instead of leaving the other ranks waiting in it."""
