@@ -893,6 +893,9 @@ def test_ranks_with_different_budgets_agree_on_exchange_sizes(tmp_path):
         assert (o["distinct"], o["generated"]) == (g["distinct"], g["generated"])
         moved += json.loads(o["info"])["rebalanced_rows"]
     assert moved > 4 * 16  # the re-balancing ran, in several sub-rounds of the agreed 16 rows
+
+
+def test_ranks_recover_fails_on_every_rank(tmp_path):
     """One rank's checkpoint file is missing: rtla_recover fails on EVERY rank
     and returns promptly -- the local failure travels in the cross-rank
     consistency reduction instead of leaving the other ranks waiting in it."""
